@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 3-D heat diffusion, 512^3 Float64 per GPU, weak scaling.
+
+Metric (BASELINE.json): effective memory throughput T_eff = A_eff / t_it with
+A_eff = 3 * n_local * sizeof(T) (T read, Cp read, T2 written) per GPU, and the
+weak-scaling efficiency E(N) = t_it(1)/t_it(N) (computed by the driver from the
+per-N values). ``value`` is the WHOLE-JOB aggregate T_eff (sum over GPUs).
+``vs_baseline`` compares the per-GPU T_eff with the reference's derived
+23 GB/s per GPU (8x P100, 256^3/GPU diffusion example).
+
+One process per GPU (torchrun); each rank owns a 512^3 block; the process
+topology comes from init_global_grid (2 GPUs -> 2x1x1, 4 -> 2x2x1,
+8 -> 2x2x2); every step = fused stencil + update_halo_ (overlapped).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n 512]
+                       [--dtype float64] [--no-overlap] [--variant V|auto]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
+METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
+          "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=512, help="local grid points per dimension")
+    ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
+    ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    import torch
+
+    import igg
+    from igg.models.diffusion3d import Diffusion3D, t_eff_gbs
+
+    if args.variant is not None:
+        os.environ["IGG_STENCIL_VARIANT"] = str(args.variant)
+    dtype = getattr(torch, args.dtype)
+    n = args.n
+    per = 1 if args.periodic else 0
+    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, n, periodx=per, periody=per, periodz=per,
+                                                         quiet=True)
+    model = Diffusion3D(dtype=dtype, overlap=not args.no_overlap)
+    for _ in range(args.warmup):
+        model.step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    # MAX over ranks (gloo all-reduce of one double)
+    el = torch.tensor([elapsed], dtype=torch.float64)
+    if nprocs > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=comm.gloo)
+    elapsed = float(el.item())
+    t_it = elapsed / args.steps
+    per_gpu = t_eff_gbs(model, t_it)
+    total = per_gpu * nprocs
+    finite = bool(torch.isfinite(model.T).all().item())
+    if me == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(total, 3),
+            "unit": "GB/s",
+            "n_gpus": nprocs,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_it * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(per_gpu / BASELINE_PER_GPU_GBS, 3),
+            "dtype": "fp64" if dtype == torch.float64 else "fp32",
+            "data": "synthetic (Gaussian-anomaly initial conditions, reference example physics)",
+            "config": {
+                "model": "diffusion3d",
+                "global_batch": nprocs,
+                "seq_len": n,
+                "parallelism": f"spatial {dims[0]}x{dims[1]}x{dims[2]}",
+                "local_grid": [n, n, n],
+                "global_grid": [int(v) for v in igg.get_global_grid().nxyz_g],
+                "overlap_comm": bool(model.overlap),
+                "t_eff_per_gpu_GBs": round(per_gpu, 3),
+                "a_eff_bytes_per_gpu": model.a_eff_bytes,
+                "transport": os.environ.get("IGG_TRANSPORT", "rccl") if nprocs > 1 else "none",
+                "stencil_variant": os.environ.get("IGG_STENCIL_VARIANT", "0"),
+                "finite": finite,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    igg.finalize_global_grid()
+
+
+if __name__ == "__main__":
+    main()

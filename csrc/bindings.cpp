@@ -1,0 +1,313 @@
+// pybind11 bindings of the native IGG runtime (_igg_native).
+//
+// The Python layer passes raw pointers, extents and strides of torch tensors
+// (CPU or HIP) plus the current HIP stream handle; nothing here links libtorch,
+// so the runtime is a self-contained C++/HIP library with a thin binding.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "igg/comm.hpp"
+#include "igg/copy.hpp"
+#include "igg/gather.hpp"
+#include "igg/halo.hpp"
+#include "igg/stencil.hpp"
+#include "igg/topology.hpp"
+
+namespace py = pybind11;
+using namespace igg;
+
+namespace {
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+using FieldTuple = std::tuple<uintptr_t, int, std::array<int64_t, 3>, std::array<int64_t, 3>, int, bool>;
+
+Field to_field(const FieldTuple& t) {
+  Field f;
+  f.ptr = std::get<0>(t);
+  f.ndims = std::get<1>(t);
+  f.size = std::get<2>(t);
+  f.stride = std::get<3>(t);
+  f.elem_bytes = std::get<4>(t);
+  f.device = std::get<5>(t);
+  return f;
+}
+
+std::vector<Field> to_fields(const std::vector<FieldTuple>& ts) {
+  std::vector<Field> fs;
+  fs.reserve(ts.size());
+  for (const auto& t : ts) fs.push_back(to_field(t));
+  return fs;
+}
+
+GridInfo make_grid(int64_t me, int64_t nprocs, const Int3& nxyz, const Int3& overlaps,
+                   const std::array<Int3, 2>& neighbors) {
+  GridInfo g;
+  g.me = me;
+  g.nprocs = nprocs;
+  g.nxyz = nxyz;
+  g.overlaps = overlaps;
+  g.neighbors = neighbors;
+  return g;
+}
+
+// Transport implemented in Python (torch.distributed gloo/nccl point-to-point).
+class PyTransport : public Transport {
+ public:
+  PyTransport(py::function fn, bool host, bool dev, std::string name)
+      : fn_(std::move(fn)), host_(host), dev_(dev), name_(std::move(name)) {}
+  bool device_capable() const override { return dev_; }
+  bool host_capable() const override { return host_; }
+  std::string name() const override { return name_; }
+  void exchange(const std::vector<P2POp>& recvs, const std::vector<P2POp>& sends, bool device,
+                hipStream_t stream) override {
+    auto conv = [](const std::vector<P2POp>& ops) {
+      py::list l;
+      for (const auto& o : ops)
+        l.append(py::make_tuple(reinterpret_cast<uintptr_t>(o.ptr), o.bytes, o.peer, o.tag));
+      return l;
+    };
+    fn_(conv(recvs), conv(sends), device, reinterpret_cast<uintptr_t>(stream));
+  }
+
+ private:
+  py::function fn_;
+  bool host_, dev_;
+  std::string name_;
+};
+
+// Pre-converted field list: the update_halo hot path converts tuples once per
+// plan, not per call.
+struct FieldSet {
+  std::vector<Field> f;
+};
+
+std::vector<Box> to_boxes(const std::vector<std::pair<Int3, Int3>>& bs) {
+  std::vector<Box> out;
+  for (const auto& b : bs) {
+    Box x;
+    for (int d = 0; d < 3; ++d) { x.lo[d] = b.first[d]; x.hi[d] = b.second[d]; }
+    out.push_back(x);
+  }
+  return out;
+}
+
+std::pair<Int3, Int3> from_box(const Box& b) {
+  return {{b.lo[0], b.lo[1], b.lo[2]}, {b.hi[0], b.hi[1], b.hi[2]}};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_igg_native, m) {
+  m.doc() = "Native MI355X runtime of the implicit global grid (HIP kernels + RCCL).";
+  py::register_exception<Error>(m, "IGGError", PyExc_RuntimeError);
+
+  m.attr("PROC_NULL") = PROC_NULL;
+  m.attr("NDIMS") = NDIMS;
+  m.attr("NNEIGHBORS") = NNEIGHBORS;
+  m.attr("ALLOC_GRANULARITY") = ALLOC_GRANULARITY;
+  m.attr("THREADCOPY_THRESHOLD") = THREADCOPY_THRESHOLD;
+
+  // --- topology
+  m.def("dims_create", &dims_create, py::arg("nprocs"), py::arg("dims"));
+  m.def("cart_coords", &cart_coords, py::arg("rank"), py::arg("dims"));
+  m.def("cart_rank", &cart_rank, py::arg("coords"), py::arg("dims"));
+  m.def("cart_shift", &cart_shift, py::arg("rank"), py::arg("dim"), py::arg("disp"),
+        py::arg("dims"), py::arg("periods"));
+  m.def("global_size", &global_size);
+  m.def("coord_g", &coord_g);
+
+  // --- device
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("set_device", [](int d) { IGG_HIP_CHECK(hipSetDevice(d)); });
+  m.def("get_device", []() {
+    int d = 0;
+    IGG_HIP_CHECK(hipGetDevice(&d));
+    return d;
+  });
+  m.def("device_synchronize", []() {
+    py::gil_scoped_release nogil;
+    IGG_HIP_CHECK(hipDeviceSynchronize());
+  });
+  m.def("stream_synchronize", [](uintptr_t s) {
+    py::gil_scoped_release nogil;
+    IGG_HIP_CHECK(hipStreamSynchronize(as_stream(s)));
+  });
+  m.def("memcpy_d2h", [](uintptr_t src, size_t n) {
+    std::string out(n, '\0');
+    IGG_HIP_CHECK(hipMemcpy(out.data(), reinterpret_cast<void*>(src), n, hipMemcpyDeviceToHost));
+    return py::bytes(out);
+  });
+  m.def("rccl_version", &rccl_version);
+
+  // --- field geometry helpers (test hooks)
+  m.def("ol", [](const GridInfo& g, int dim, const FieldTuple& f) { return ol(g, dim, to_field(f)); });
+  m.def("max_halo_elems", [](const FieldTuple& f) { return max_halo_elems(to_field(f)); });
+  m.def("send_index", [](const GridInfo& g, int side, int dim, const FieldTuple& f) {
+    return send_index(g, side, dim, to_field(f));
+  });
+  m.def("recv_index", [](const GridInfo& g, int side, int dim, const FieldTuple& f) {
+    return recv_index(g, side, dim, to_field(f));
+  });
+  m.def("face_info", [](const FieldTuple& f, int dim, int64_t index) {
+    const Face fc = face(to_field(f), dim, index);
+    return py::make_tuple(reinterpret_cast<uintptr_t>(fc.base), fc.n_outer, fc.n_inner, fc.s_outer,
+                          fc.s_inner, fc.contiguous, fc.bytes);
+  });
+
+  py::class_<GridInfo>(m, "GridInfo")
+      .def(py::init(&make_grid), py::arg("me"), py::arg("nprocs"), py::arg("nxyz"),
+           py::arg("overlaps"), py::arg("neighbors"))
+      .def_readwrite("me", &GridInfo::me)
+      .def_readwrite("nprocs", &GridInfo::nprocs)
+      .def_readwrite("nxyz", &GridInfo::nxyz)
+      .def_readwrite("overlaps", &GridInfo::overlaps)
+      .def_readwrite("neighbors", &GridInfo::neighbors);
+
+  // --- copies
+  m.def("copy2d",
+        [](const std::vector<std::tuple<uintptr_t, uintptr_t, int64_t, int64_t, int64_t, int64_t,
+                                        int64_t, int64_t>>& cs,
+           int elem_bytes, bool device, uintptr_t stream) {
+          std::vector<Copy2D> v;
+          for (const auto& c : cs)
+            v.push_back({reinterpret_cast<const char*>(std::get<0>(c)),
+                         reinterpret_cast<char*>(std::get<1>(c)), std::get<2>(c), std::get<3>(c),
+                         std::get<4>(c), std::get<5>(c), std::get<6>(c), std::get<7>(c)});
+          if (device) launch_copy2d(v, elem_bytes, as_stream(stream));
+          else host_copy2d(v, elem_bytes);
+        });
+
+  // --- transports
+  py::class_<Transport, std::shared_ptr<Transport>>(m, "Transport")
+      .def_property_readonly("name", &Transport::name)
+      .def_property_readonly("device_capable", &Transport::device_capable)
+      .def_property_readonly("host_capable", &Transport::host_capable);
+  py::class_<PyTransport, Transport, std::shared_ptr<PyTransport>>(m, "PyTransport")
+      .def(py::init<py::function, bool, bool, std::string>(), py::arg("fn"), py::arg("host"),
+           py::arg("device"), py::arg("name"));
+  py::class_<RcclComm, Transport, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def_static("unique_id", []() {
+        auto v = RcclComm::unique_id();
+        return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+      })
+      .def(py::init([](py::bytes uid, int nranks, int rank) {
+             std::string s = uid;
+             std::vector<uint8_t> v(s.begin(), s.end());
+             py::gil_scoped_release nogil;  // blocking rendezvous
+             return std::make_shared<RcclComm>(v, nranks, rank);
+           }),
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"))
+      .def("barrier", [](RcclComm& c, uintptr_t s) { c.barrier(as_stream(s)); })
+      .def("check_async_error", &RcclComm::check_async_error)
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def("p2p",
+           [](RcclComm& c, const std::vector<std::tuple<uintptr_t, size_t, int>>& recvs,
+              const std::vector<std::tuple<uintptr_t, size_t, int>>& sends, uintptr_t s) {
+             std::vector<P2POp> r, sd;
+             for (const auto& x : recvs)
+               r.push_back({reinterpret_cast<void*>(std::get<0>(x)), std::get<1>(x), std::get<2>(x), 0});
+             for (const auto& x : sends)
+               sd.push_back({reinterpret_cast<void*>(std::get<0>(x)), std::get<1>(x), std::get<2>(x), 0});
+             c.exchange(r, sd, true, as_stream(s));
+           });
+
+  // --- halo engine
+  py::class_<FieldSet>(m, "FieldSet")
+      .def(py::init([](const std::vector<FieldTuple>& ts) { return FieldSet{to_fields(ts)}; }))
+      .def("__len__", [](const FieldSet& s) { return s.f.size(); });
+  py::class_<HaloEngine>(m, "HaloEngine")
+      .def(py::init<const GridInfo&>())
+      .def_property_readonly("grid", [](HaloEngine& e) { return e.grid(); })
+      .def("set_grid", [](HaloEngine& e, const GridInfo& g) { e.grid() = g; })
+      .def("set_transport", &HaloEngine::set_transport, py::arg("transport"), py::arg("device"))
+      .def("clear_transport", [](HaloEngine& e, bool device) { e.set_transport(nullptr, device); })
+      .def("transport_name", [](HaloEngine& e, bool device) {
+        auto t = e.transport(device);
+        return t ? t->name() : std::string("none");
+      })
+      .def("exchange",
+           [](HaloEngine& e, const std::vector<FieldTuple>& fs, uintptr_t s) {
+             e.exchange(to_fields(fs), as_stream(s));
+           })
+      .def("exchange_set",
+           [](HaloEngine& e, const FieldSet& fs, uintptr_t s) { e.exchange(fs.f, as_stream(s)); })
+      .def("exchange_dim",
+           [](HaloEngine& e, const std::vector<FieldTuple>& fs, int dim, uintptr_t s) {
+             e.exchange_dim(to_fields(fs), dim, as_stream(s));
+           })
+      .def("pool_ensure",
+           [](HaloEngine& e, const std::vector<FieldTuple>& fs, bool device) {
+             e.pool().ensure(to_fields(fs), device);
+           })
+      .def("pool_free", [](HaloEngine& e) { e.pool().free_all(); })
+      .def("pool_allocated", [](HaloEngine& e, bool device) { return e.pool().allocated(device); })
+      .def("pool_nslots", [](HaloEngine& e, bool device) { return e.pool().nslots(device); })
+      .def("pool_capacity",
+           [](HaloEngine& e, size_t slot, bool device) { return e.pool().capacity(slot, device); })
+      .def("pool_ptrs", [](HaloEngine& e, size_t slot, bool device) {
+        auto& p = e.pool();
+        return py::make_tuple(reinterpret_cast<uintptr_t>(p.send(slot, 0, device)),
+                              reinterpret_cast<uintptr_t>(p.send(slot, 1, device)),
+                              reinterpret_cast<uintptr_t>(p.recv(slot, 0, device)),
+                              reinterpret_cast<uintptr_t>(p.recv(slot, 1, device)));
+      });
+
+  // --- gather
+  py::class_<Gatherer>(m, "Gatherer")
+      .def(py::init<>())
+      .def("gather",
+           [](Gatherer& g, const FieldTuple& a, uintptr_t dst, int root, const Int3& dims,
+              RcclComm& comm, uintptr_t s) {
+             g.gather(to_field(a), reinterpret_cast<void*>(dst), root, dims, comm, as_stream(s));
+           })
+      .def("free", &Gatherer::free)
+      .def_property_readonly("capacity", &Gatherer::capacity);
+  m.def("gather_reorder", [](uintptr_t src, uintptr_t dst, const Int3& s, const Int3& dims,
+                             int eb, uintptr_t stream) {
+    launch_gather_reorder(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), s, dims,
+                          eb, as_stream(stream));
+  });
+
+  // --- stencils
+  m.def("diffusion3d_variants", []() {
+    std::vector<std::string> v;
+    for (int i = 0; i < diffusion3d_num_variants(); ++i) v.push_back(diffusion3d_variant_name(i));
+    return v;
+  });
+  m.def("diffusion3d",
+        [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
+           double dtlam, int elem_bytes, const std::vector<std::pair<Int3, Int3>>& boxes,
+           bool device, int variant, uintptr_t stream) {
+          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes};
+          const auto bx = to_boxes(boxes);
+          if (device) {
+            launch_diffusion3d(a, bx, variant, as_stream(stream));
+          } else {
+            py::gil_scoped_release nogil;
+            host_diffusion3d(a, bx);
+          }
+        },
+        py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
+        py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
+        py::arg("stream") = 0);
+  m.def("split_boundary", [](const Int3& n, const std::array<bool, 3>& active, const Int3& w) {
+    std::vector<Box> slabs;
+    Box interior;
+    int64_t nn[3] = {n[0], n[1], n[2]}, ww[3] = {w[0], w[1], w[2]};
+    bool aa[3] = {active[0], active[1], active[2]};
+    split_boundary(nn, aa, ww, slabs, interior);
+    std::vector<std::pair<Int3, Int3>> out;
+    for (const Box& b : slabs) out.push_back(from_box(b));
+    return py::make_tuple(out, from_box(interior));
+  });
+}

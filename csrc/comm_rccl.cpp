@@ -1,0 +1,81 @@
+// RCCL transport (see include/igg/comm.hpp).
+#include <cstring>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "igg/comm.hpp"
+
+#define IGG_NCCL_CHECK(expr)                                                        \
+  do {                                                                              \
+    ncclResult_t _r = (expr);                                                       \
+    if (_r != ncclSuccess)                                                          \
+      ::igg::fail("RCCL error '", ncclGetErrorString(_r), "' at ", __FILE__, ":",   \
+                  __LINE__, " in ", #expr);                                         \
+  } while (0)
+
+namespace igg {
+
+static_assert(sizeof(ncclUniqueId) == RcclComm::UID_BYTES, "unexpected ncclUniqueId size");
+
+std::vector<uint8_t> RcclComm::unique_id() {
+  ncclUniqueId id;
+  IGG_NCCL_CHECK(ncclGetUniqueId(&id));
+  std::vector<uint8_t> out(sizeof(id));
+  std::memcpy(out.data(), &id, sizeof(id));
+  return out;
+}
+
+RcclComm::RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank)
+    : rank_(rank), nranks_(nranks) {
+  if (uid.size() != sizeof(ncclUniqueId)) fail("RcclComm: bad unique id size ", uid.size());
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  IGG_NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+  IGG_HIP_CHECK(hipMalloc(&scratch_, 256));
+  IGG_HIP_CHECK(hipMemset(scratch_, 0, 256));
+}
+
+RcclComm::~RcclComm() {
+  if (scratch_) (void)hipFree(scratch_);
+  if (comm_ && !aborted_) (void)ncclCommDestroy(comm_);
+}
+
+void RcclComm::exchange(const std::vector<P2POp>& recvs, const std::vector<P2POp>& sends,
+                        bool device, hipStream_t stream) {
+  if (!device) fail("RCCL transport can only move device (GPU) memory.");
+  if (recvs.empty() && sends.empty()) return;
+  IGG_NCCL_CHECK(ncclGroupStart());
+  for (const P2POp& r : recvs)
+    IGG_NCCL_CHECK(ncclRecv(r.ptr, r.bytes, ncclUint8, r.peer, comm_, stream));
+  for (const P2POp& s : sends)
+    IGG_NCCL_CHECK(ncclSend(s.ptr, s.bytes, ncclUint8, s.peer, comm_, stream));
+  IGG_NCCL_CHECK(ncclGroupEnd());
+}
+
+void RcclComm::barrier(hipStream_t stream) {
+  IGG_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, stream));
+}
+
+void RcclComm::check_async_error() {
+  ncclResult_t st = ncclSuccess;
+  IGG_NCCL_CHECK(ncclCommGetAsyncError(comm_, &st));
+  if (st != ncclSuccess && st != ncclInProgress)
+    fail("RCCL asynchronous error: ", ncclGetErrorString(st));
+}
+
+void RcclComm::abort() {
+  if (comm_ && !aborted_) {
+    (void)ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}
+
+std::string rccl_version() {
+  int v = 0;
+  if (ncclGetVersion(&v) != ncclSuccess) return "unknown";
+  return std::to_string(v / 10000) + "." + std::to_string((v / 100) % 100) + "." +
+         std::to_string(v % 100);
+}
+
+}  // namespace igg

@@ -1,0 +1,47 @@
+// Batched strided 2-D copies: the single primitive behind halo pack, unpack,
+// in-place self-periodic exchange and gather reorder.
+//
+// Reference equivalents: write_d2x!/read_x2d! GPU kernels
+// (src/update_halo.jl:655-678), write_h2h!/read_h2h! + memcopy! host copies
+// (src/update_halo.jl:569-596, 755-784) and gpumemcopy! (:796-798). Unlike the
+// reference (one 32-lane launch per field and side), one launch here moves every
+// face of every field of a dimension.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+
+#include "igg/common.hpp"
+
+namespace igg {
+
+// One strided 2-D copy of n_outer x n_inner elements; strides are in elements.
+struct Copy2D {
+  const char* src;
+  char* dst;
+  int64_t n_outer, n_inner;
+  int64_t src_so, src_si;
+  int64_t dst_so, dst_si;
+};
+
+constexpr int MAX_BATCH = 24;  // keeps the kernel argument block < 4 KiB
+
+struct CopyBatch {
+  Copy2D c[MAX_BATCH];
+  int64_t block_start[MAX_BATCH + 1];
+  int n;
+};
+
+// Device: enqueue all copies (any count, split in MAX_BATCH chunks) on `stream`.
+void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream);
+
+// Host: perform all copies now (threaded above THREADCOPY_THRESHOLD bytes).
+void host_copy2d(const std::vector<Copy2D>& copies, int elem_bytes);
+
+// Host parallel-for on the runtime's persistent worker pool.
+void host_parallel_for(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn);
+
+}  // namespace igg

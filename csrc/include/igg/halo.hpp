@@ -1,0 +1,122 @@
+// Halo exchange engine.
+//
+// Reference behaviour reproduced (ImplicitGlobalGrid.jl):
+//   * ol(dim,A) = overlaps[dim] + size(A,dim) - nxyz[dim]; a field has a halo in
+//     `dim` iff ol >= 2 (src/shared.jl:94, src/update_halo.jl:370,429,809).
+//   * The halo is one plane per side whatever the overlap; send planes are
+//     ol-1 (left) and size-ol (right), receive planes 0 and size-1, 0-based
+//     (sendranges/recvranges, src/update_halo.jl:544-563).
+//   * Dimensions are processed strictly x -> y -> z; each face spans the full
+//     extent of the other dimensions so edges/corners come out right without
+//     diagonal messages (src/update_halo.jl:40).
+//   * Missing neighbours (PROC_NULL) are skipped; a dimension whose two
+//     neighbours are this rank is exchanged locally (src/update_halo.jl:57-63);
+//     one-sided self neighbours are an error (:64-65).
+//   * Buffers: one send + one recv buffer per field position and side, sized by
+//     the largest face (product of all but the smallest extent), rounded up to
+//     32 elements, grow-only, reused across dimensions and element types
+//     (src/update_halo.jl:150-210).
+// MI355X-first differences: all faces of a dimension are packed by ONE kernel
+// launch, moved by ONE RCCL group, unpacked by ONE launch; contiguous faces are
+// sent/received in place (zero-copy, no pack/unpack); the self-periodic case is
+// ONE in-place plane-copy launch with no buffers; everything is stream-ordered
+// (no host synchronisation), so an exchange can be captured in a hipGraph.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+
+#include "igg/comm.hpp"
+#include "igg/copy.hpp"
+#include "igg/topology.hpp"
+
+namespace igg {
+
+struct Field {
+  uintptr_t ptr = 0;
+  int ndims = 0;
+  Int3 size{1, 1, 1};
+  Int3 stride{1, 1, 1};  // in elements
+  int elem_bytes = 0;
+  bool device = false;
+};
+
+struct GridInfo {
+  int64_t me = 0, nprocs = 1;
+  Int3 nxyz{1, 1, 1};
+  Int3 overlaps{2, 2, 2};
+  std::array<Int3, NNEIGHBORS> neighbors{{{PROC_NULL, PROC_NULL, PROC_NULL},
+                                          {PROC_NULL, PROC_NULL, PROC_NULL}}};
+};
+
+// A face (one plane of a field orthogonal to `dim`) as a strided 2-D region.
+struct Face {
+  char* base;
+  int64_t n_outer, n_inner, s_outer, s_inner;
+  bool contiguous;
+  size_t bytes;
+};
+
+int64_t ol(const GridInfo& g, int dim, const Field& f);
+int64_t max_halo_elems(const Field& f);
+int64_t send_index(const GridInfo& g, int side, int dim, const Field& f);
+int64_t recv_index(const GridInfo& g, int side, int dim, const Field& f);
+Face face(const Field& f, int dim, int64_t index);
+
+// Grow-only per (field slot, side) send/recv byte buffers; separate host and
+// device pools (test hooks: capacities are observable).
+class BufferPool {
+ public:
+  ~BufferPool();
+  void ensure(const std::vector<Field>& fields, bool device);
+  char* send(size_t slot, int side, bool device) const;
+  char* recv(size_t slot, int side, bool device) const;
+  size_t nslots(bool device) const { return (device ? dev_ : host_).size(); }
+  size_t capacity(size_t slot, bool device) const;
+  bool allocated(bool device) const { return device ? dev_alloc_ : host_alloc_; }
+  void free_all();
+
+ private:
+  struct Buf { char* p = nullptr; size_t bytes = 0; };
+  struct Slot { Buf send[NNEIGHBORS], recv[NNEIGHBORS]; };
+  void grow(Buf& b, size_t bytes, bool device);
+  void release(Buf& b, bool device);
+  std::vector<Slot> host_, dev_;
+  bool host_alloc_ = false, dev_alloc_ = false;
+};
+
+class HaloEngine {
+ public:
+  explicit HaloEngine(const GridInfo& g);
+  ~HaloEngine();
+  // Transports for host (CPU) and device (GPU) fields respectively.
+  void set_transport(std::shared_ptr<Transport> t, bool device) {
+    (device ? dev_transport_ : host_transport_) = std::move(t);
+  }
+  std::shared_ptr<Transport> transport(bool device) const {
+    return device ? dev_transport_ : host_transport_;
+  }
+  GridInfo& grid() { return grid_; }
+  BufferPool& pool() { return pool_; }
+
+  // Full update_halo! of `fields` (validated by the caller), stream-ordered.
+  void exchange(const std::vector<Field>& fields, hipStream_t stream);
+  // Only the dimension `dim` (0-based); used by tests and pipelined apps.
+  void exchange_dim(const std::vector<Field>& fields, int dim, hipStream_t stream);
+
+ private:
+  void exchange_dim_impl(const std::vector<Field>& fields, int dim, bool device,
+                         hipStream_t stream);
+  GridInfo grid_;
+  BufferPool pool_;
+  std::shared_ptr<Transport> host_transport_, dev_transport_;
+  hipEvent_t done_ = nullptr;
+  hipStream_t last_stream_ = nullptr;
+  bool have_event_ = false;
+};
+
+}  // namespace igg

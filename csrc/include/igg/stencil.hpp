@@ -1,0 +1,49 @@
+// Fused stencil kernels of the benchmark applications.
+//
+// 3-D heat diffusion (examples/diffusion3D_multigpu_CuArrays_novis.jl:42-46):
+// the reference runs 5 broadcast kernels per step through 4 temporaries
+// (qx, qy, qz, dTedt). Fused here into one pass:
+//   T2 = T + dt*lam/Cp * (d2T/dx2 + d2T/dy2 + d2T/dz2)       (interior points)
+// with ping-pong T/T2 and no temporaries, so the compulsory traffic is exactly
+// A_eff = 3 arrays (read T, read Cp, write T2). The update region is a list of
+// boxes so the same kernel computes boundary slabs (on the high-priority halo
+// stream, ahead of the exchange) and the interior (on the compute stream).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+
+#include "igg/common.hpp"
+
+namespace igg {
+
+struct Box {
+  int64_t lo[3], hi[3];  // half-open index ranges along dims 0,1,2
+  bool empty() const { return lo[0] >= hi[0] || lo[1] >= hi[1] || lo[2] >= hi[2]; }
+};
+
+struct DiffusionArgs {
+  uintptr_t t2, t, cp;      // C-contiguous (n0,n1,n2) arrays, dim 2 fastest
+  int64_t n[3];
+  double rd2[3];            // 1/dx_d^2
+  double dt_lam;            // dt*lam
+  int elem_bytes;           // 8 (f64) or 4 (f32)
+};
+
+// Number of tuned kernel variants (see stencil_kernels.hip); variant 0 = default.
+int diffusion3d_num_variants();
+const char* diffusion3d_variant_name(int v);
+
+void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, int variant,
+                        hipStream_t stream);
+void host_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes);
+
+// Boundary-slab / interior decomposition of the inner box [1,n-1)^3.
+// Along each dim with `active[d]`, slabs of width w[d] at both ends are split
+// off (they hold the planes that update_halo sends). Returns {slabs, interior}.
+void split_boundary(const int64_t n[3], const bool active[3], const int64_t w[3],
+                    std::vector<Box>& slabs, Box& interior);
+
+}  // namespace igg

@@ -1,0 +1,116 @@
+"""3-D heat diffusion with Gaussian-anomaly initial conditions (the benchmark).
+
+Reference application: examples/diffusion3D_multigpu_CuArrays_novis.jl (and its
+CPU twin diffusion3D_multicpu_novis.jl): lam=1, cp_min=1, l=10 per axis, two
+Gaussian anomalies in Cp and two in T built from x_g/y_g/z_g,
+dt = min(dx^2,dy^2,dz^2)*cp_min/lam/8.1, per step: stencil update of the
+interior then ``update_halo!(T)``.
+
+MI355X design of a time step (``overlap=True`` and at least one neighbour):
+
+  halo stream (high priority): boundary slabs of T2 (the planes update_halo
+      sends) -> update_halo_(T2)  [pack -> RCCL -> unpack, x->y->z]
+  compute stream:              interior of T2 (everything else)
+  join, swap T <-> T2.
+
+Both read T only; they write disjoint parts of T2, so the exchange hides behind
+the interior update. Without neighbours (1 GPU, non-periodic) the step is one
+fused kernel and update_halo_ is a no-op, as in the reference.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import parallel  # noqa: F401
+from ..ops import stencil
+from ..parallel import grid as _grid
+from ..parallel.halo import update_halo_
+from ..utils.tools import coords_g, nx_g, ny_g, nz_g
+
+
+class Diffusion3D:
+    def __init__(self, *, dtype=torch.float64, device=None, lam: float = 1.0, cp_min: float = 1.0,
+                 lx: float = 10.0, ly: float = 10.0, lz: float = 10.0, overlap: bool = True,
+                 slab_width=None, variant=None):
+        gg = _grid.global_grid()
+        nx, ny, nz = (int(v) for v in gg.nxyz)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if gg.amdgpu_enabled else torch.device("cpu")
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.lam, self.cp_min = lam, cp_min
+        self.dx = lx / (nx_g() - 1)
+        self.dy = ly / (ny_g() - 1)
+        self.dz = lz / (nz_g() - 1)
+        self.dt = min(self.dx ** 2, self.dy ** 2, self.dz ** 2) * cp_min / lam / 8.1
+        self.variant = variant
+        shape = (nx, ny, nz)
+        probe = torch.empty(shape, device="meta")  # sizes only, for coords_g
+        kw = dict(dtype=torch.float64, device=self.device)
+        x = coords_g(0, self.dx, probe, **kw).view(-1, 1, 1)
+        y = coords_g(1, self.dy, probe, **kw).view(1, -1, 1)
+        z = coords_g(2, self.dz, probe, **kw).view(1, 1, -1)
+        self.Cp = (cp_min + 5 * torch.exp(-(x - lx / 1.5) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2)
+                   + 5 * torch.exp(-(x - lx / 3.0) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2)).to(dtype).contiguous()
+        self.T = (100 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 3.0) / 2) ** 2)
+                  + 50 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 1.5) / 2) ** 2)).to(dtype).contiguous()
+        self.T2 = self.T.clone()
+        active = [bool((gg.neighbors[:, d] != -1).any()) for d in range(3)]
+        self.overlap = overlap and self.device.type == "cuda" and any(active)
+        if slab_width is None:
+            # dim-2 slabs span one 128-B line so interior rows stay line-aligned.
+            slab_width = (1, 1, 128 // torch.empty(0, dtype=dtype).element_size() - 1)
+        self.slabs, self.interior = stencil.split_boundary(shape, active, slab_width)
+        self.inner = [stencil.inner_box(shape)]
+        if self.overlap:
+            _least, greatest = torch.cuda.Stream.priority_range()
+            self.halo_stream = torch.cuda.Stream(device=self.device, priority=greatest)
+
+    def _kw(self):
+        return dict(lam=self.lam, dt=self.dt, dx=self.dx, dy=self.dy, dz=self.dz, variant=self.variant)
+
+    def step(self) -> None:
+        """Advance one time step (T <- T2 after the update and halo exchange)."""
+        T, T2, Cp = self.T, self.T2, self.Cp
+        if self.overlap:
+            main = torch.cuda.current_stream()
+            hs = self.halo_stream
+            hs.wait_stream(main)
+            with torch.cuda.stream(hs):
+                stencil.diffusion3d_(T2, T, Cp, boxes=self.slabs, **self._kw())
+                update_halo_(T2)
+            stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw())
+            main.wait_stream(hs)
+        else:
+            stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
+            update_halo_(T2)
+        self.T, self.T2 = T2, T
+
+    def run(self, nt: int) -> None:
+        for _ in range(nt):
+            self.step()
+
+    @property
+    def a_eff_bytes(self) -> int:
+        """A_eff = (2*D_u + D_k) * n_local * sizeof(T) with D_u = D_k = 1."""
+        return 3 * self.T.numel() * self.T.element_size()
+
+
+def t_eff_gbs(model: Diffusion3D, t_it: float) -> float:
+    return model.a_eff_bytes / t_it / 1e9
+
+
+def run_diffusion3d(nx=128, ny=128, nz=128, nt=100, **kw):
+    """Example driver mirroring diffusion3D_multicpu_novis.jl / _multigpu_ (novis)."""
+    from ..parallel.grid import finalize_global_grid, init_global_grid
+    from ..utils.tools import tic, toc
+
+    init_global_grid(nx, ny, nz, quiet=kw.pop("quiet", False))
+    m = Diffusion3D(**kw)
+    tic()
+    m.run(nt)
+    t = toc()
+    finalize_global_grid()
+    return m, t

@@ -1,0 +1,114 @@
+"""Stencil operators backed by the native kernels (csrc/kernels/stencil_kernels.hip).
+
+``diffusion3d_`` computes one explicit heat-diffusion update of the interior
+(or of a list of boxes inside it) in a single fused pass:
+
+    T2 = T + dt*lam/Cp * (d2T/dx2 + d2T/dy2 + d2T/dz2)
+
+which is the five broadcast kernels of the reference example
+(examples/diffusion3D_multigpu_CuArrays_novis.jl:42-46) fused, with no
+temporaries. GPU tensors run the hand-written HIP kernel on the current stream;
+CPU tensors run the threaded C++ host kernel.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .._native import IGGError, native
+
+_autotune_cache: dict = {}
+
+
+def variants() -> list[str]:
+    return list(native.diffusion3d_variants())
+
+
+def _check(T2, T, Cp):
+    for name, A in (("T2", T2), ("T", T), ("Cp", Cp)):
+        if A.dim() != 3:
+            raise IGGError(f"diffusion3d: {name} must be 3-D")
+        if not A.is_contiguous():
+            raise IGGError(f"diffusion3d: {name} must be C-contiguous")
+        if A.shape != T.shape or A.dtype != T.dtype or A.device != T.device:
+            raise IGGError("diffusion3d: T2, T and Cp must have identical shape, dtype and device")
+    if T.dtype not in (torch.float32, torch.float64):
+        raise IGGError("diffusion3d: only float32 and float64 are supported")
+    if T2.data_ptr() == T.data_ptr():
+        raise IGGError("diffusion3d: T2 must not alias T (use ping-pong buffers)")
+
+
+def inner_box(shape) -> tuple:
+    return ((1, 1, 1), tuple(int(s) - 1 for s in shape))
+
+
+def _variant_for(T, boxes, rd2, dtlam, T2, Cp, stream) -> int:
+    env = os.environ.get("IGG_STENCIL_VARIANT", "0").strip().lower()
+    if env != "auto":
+        return int(env)
+    key = (tuple(T.shape), T.dtype, tuple(map(tuple, (b[0] for b in boxes))), tuple(map(tuple, (b[1] for b in boxes))))
+    v = _autotune_cache.get(key)
+    if v is None:
+        v = autotune(T2, T, Cp, rd2, dtlam, boxes)
+        _autotune_cache[key] = v
+    return v
+
+
+def autotune(T2, T, Cp, rd2, dtlam, boxes, reps: int = 5) -> int:
+    """Time every kernel variant on these arrays (the update is pure: T2 = f(T, Cp))."""
+    n = list(T.shape)
+    best, best_t = 0, float("inf")
+    s = torch.cuda.current_stream()
+    for v in range(len(variants())):
+        args = (T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(), boxes, True, v, s.cuda_stream)
+        native.diffusion3d(*args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            native.diffusion3d(*args)
+        e1.record(s)
+        e1.synchronize()
+        t = e0.elapsed_time(e1)
+        if t < best_t:
+            best, best_t = v, t
+    return best
+
+
+def diffusion3d_(T2, T, Cp, *, lam: float, dt: float, dx: float, dy: float, dz: float,
+                 boxes=None, variant: int | None = None, stream: int | None = None) -> None:
+    """One fused diffusion update of ``T2`` from ``T`` on ``boxes`` (default: whole interior)."""
+    _check(T2, T, Cp)
+    rd2 = [1.0 / (dx * dx), 1.0 / (dy * dy), 1.0 / (dz * dz)]
+    dtlam = dt * lam
+    if boxes is None:
+        boxes = [inner_box(T.shape)]
+    boxes = [(list(b[0]), list(b[1])) for b in boxes]
+    dev = T.is_cuda
+    if dev:
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        v = _variant_for(T, boxes, rd2, dtlam, T2, Cp, s) if variant is None else variant
+    else:
+        s, v = 0, 0
+    native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), list(T.shape), rd2, dtlam,
+                       T.element_size(), boxes, dev, v, s)
+
+
+def diffusion3d_reference(T, Cp, *, lam, dt, dx, dy, dz) -> torch.Tensor:
+    """Plain-PyTorch (fp64) reference of the reference example's 5 broadcasts."""
+    T = T.double()
+    Cp = Cp.double()
+    qx = -lam * (T[1:, 1:-1, 1:-1] - T[:-1, 1:-1, 1:-1]) / dx
+    qy = -lam * (T[1:-1, 1:, 1:-1] - T[1:-1, :-1, 1:-1]) / dy
+    qz = -lam * (T[1:-1, 1:-1, 1:] - T[1:-1, 1:-1, :-1]) / dz
+    dTedt = 1.0 / Cp[1:-1, 1:-1, 1:-1] * (
+        -(qx[1:] - qx[:-1]) / dx - (qy[:, 1:] - qy[:, :-1]) / dy - (qz[:, :, 1:] - qz[:, :, :-1]) / dz)
+    out = T.clone()
+    out[1:-1, 1:-1, 1:-1] = T[1:-1, 1:-1, 1:-1] + dt * dTedt
+    return out
+
+
+def split_boundary(shape, active, widths):
+    """Boundary slabs + interior box of the inner region (see csrc/stencil_host.cpp)."""
+    slabs, interior = native.split_boundary(list(shape), list(active), list(widths))
+    return slabs, interior

@@ -1,0 +1,235 @@
+"""Distributed runtime: process group, RCCL communicator and transports.
+
+Reference: MPI.jl drives all communication (src/shared.jl:1; MPI.Init in
+src/init_global_grid.jl:78-83, Finalize in src/finalize_global_grid.jl:19-23).
+MPI is not part of the MI355X stack; the replacement is
+
+* one process per GPU, started by ``torchrun`` (or any launcher exporting
+  ``RANK``/``WORLD_SIZE``/``MASTER_ADDR``/``MASTER_PORT``), bootstrapped through
+  ``torch.distributed`` (TCP store at 127.0.0.1 on one node);
+* a ``gloo`` group for host-side control traffic (barriers, the RCCL unique-id
+  broadcast, CPU-tensor halos and gathers);
+* a native RCCL communicator (``_igg_native.RcclComm``) for device-resident
+  point-to-point traffic over xGMI — grouped ncclSend/ncclRecv enqueued on HIP
+  streams by the C++ halo engine, no Python on the data path.
+
+``IGG_TRANSPORT=torch`` swaps the native RCCL transport for torch.distributed's
+``nccl`` (= RCCL) ``batch_isend_irecv`` (debug/A-B only).
+"""
+from __future__ import annotations
+
+import ctypes
+import datetime
+import os
+import socket
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from .._native import IGGError, native
+from ..utils import config
+
+
+def _host_view(ptr: int, nbytes: int) -> torch.Tensor:
+    """uint8 CPU tensor aliasing native host memory (no copy)."""
+    if nbytes == 0:
+        return torch.empty(0, dtype=torch.uint8)
+    buf = (ctypes.c_uint8 * nbytes).from_address(ptr)
+    return torch.frombuffer(buf, dtype=torch.uint8)
+
+
+class _DeviceBuf:
+    """__cuda_array_interface__ wrapper to alias a raw HIP pointer as a tensor."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {
+            "shape": (nbytes,),
+            "typestr": "|u1",
+            "data": (ptr, False),
+            "version": 3,
+        }
+
+
+def _device_view(ptr: int, nbytes: int) -> torch.Tensor:
+    return torch.as_tensor(_DeviceBuf(ptr, nbytes), device="cuda")
+
+
+def runtime_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def init_runtime(timeout_s: float = 600.0) -> None:
+    """Initialise torch.distributed (the MPI.Init equivalent).
+
+    With launcher environment variables (``WORLD_SIZE`` etc.) this joins the
+    job over ``env://``; otherwise a single-process group is created on an
+    in-memory store.
+    """
+    if runtime_initialized():
+        raise IGGError("The distributed runtime is already initialized.")
+    timeout = datetime.timedelta(seconds=timeout_s)
+    if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", init_method="env://", timeout=timeout)
+    else:
+        dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1, timeout=timeout)
+
+
+def finalize_runtime() -> None:
+    if not runtime_initialized():
+        raise IGGError("The distributed runtime cannot be finalized as it has not been initialized.")
+    dist.destroy_process_group()
+
+
+@dataclass
+class Communicator:
+    """The Cartesian communicator returned by ``init_global_grid`` (comm_cart).
+
+    ``rank``/``size`` are ranks of ``group`` (row-major Cartesian order, no
+    reordering). ``gloo`` carries host traffic; ``rccl`` device traffic.
+    """
+
+    group: object = None
+    gloo: object = None
+    rank: int = 0
+    size: int = 1
+    rccl: object = None
+    torch_nccl: object = None
+    local_rank: int = 0
+    local_size: int = 1
+    _transports: dict = field(default_factory=dict)
+
+    def __eq__(self, other):  # identity semantics like MPI.Comm handles
+        return self is other
+
+    __hash__ = object.__hash__
+
+    def global_rank(self, r: int) -> int:
+        if self.gloo is None or self.gloo == dist.GroupMember.WORLD:
+            return r
+        return dist.get_global_rank(self.gloo, r)
+
+    # -- collectives -------------------------------------------------------
+    def barrier(self) -> None:
+        if self.size > 1:
+            dist.barrier(group=self.gloo)
+
+    def broadcast_object(self, obj, root: int = 0):
+        if self.size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=self.global_rank(root), group=self.gloo)
+        return lst[0]
+
+    def all_gather_object(self, obj) -> list:
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj, group=self.gloo)
+        return out
+
+    # -- transports ----------------------------------------------------------
+    def host_transport(self):
+        t = self._transports.get("gloo")
+        if t is None:
+            t = native.PyTransport(self._gloo_p2p, True, False, "gloo")
+            self._transports["gloo"] = t
+        return t
+
+    def device_transport(self):
+        if self.size == 1:
+            return None
+        if config.transport_choice() == "torch":
+            t = self._transports.get("torch")
+            if t is None:
+                self._ensure_torch_nccl()
+                t = native.PyTransport(self._torch_p2p, False, True, "torch-nccl")
+                self._transports["torch"] = t
+            return t
+        self.ensure_rccl()
+        return self.rccl
+
+    def ensure_rccl(self):
+        if self.rccl is None and self.size > 1:
+            uid = native.RcclComm.unique_id() if self.rank == 0 else None
+            uid = self.broadcast_object(uid, root=0)
+            self.rccl = native.RcclComm(uid, self.size, self.rank)
+        return self.rccl
+
+    def _ensure_torch_nccl(self):
+        if self.torch_nccl is None:
+            ranks = [self.global_rank(r) for r in range(self.size)]
+            self.torch_nccl = dist.new_group(ranks=ranks, backend="nccl")
+
+    def _gloo_p2p(self, recvs, sends, device, stream):
+        if device:
+            raise IGGError("gloo transport cannot move GPU memory.")
+        reqs = []
+        for ptr, nbytes, peer, tag in recvs:
+            reqs.append(dist.irecv(_host_view(ptr, nbytes), src=self.global_rank(peer), group=self.gloo, tag=tag))
+        for ptr, nbytes, peer, tag in sends:
+            reqs.append(dist.isend(_host_view(ptr, nbytes), dst=self.global_rank(peer), group=self.gloo, tag=tag))
+        for r in reqs:
+            r.wait()
+
+    def _torch_p2p(self, recvs, sends, device, stream):
+        ops = []
+        for ptr, nbytes, peer, _tag in recvs:
+            ops.append(dist.P2POp(dist.irecv, _device_view(ptr, nbytes), self.global_rank(peer), self.torch_nccl))
+        for ptr, nbytes, peer, _tag in sends:
+            ops.append(dist.P2POp(dist.isend, _device_view(ptr, nbytes), self.global_rank(peer), self.torch_nccl))
+        if not ops:
+            return
+        with torch.cuda.stream(torch.cuda.ExternalStream(stream)):
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+
+    def destroy(self) -> None:
+        if self.rccl is not None:
+            try:
+                native.device_synchronize()
+            except Exception:
+                pass
+            self.rccl = None
+        self._transports.clear()
+        if self.torch_nccl is not None:
+            try:
+                dist.destroy_process_group(self.torch_nccl)
+            except Exception:
+                pass
+            self.torch_nccl = None
+        if self.gloo is not None and self.gloo is not self.group and runtime_initialized():
+            try:
+                dist.destroy_process_group(self.gloo)
+            except Exception:
+                pass
+        self.gloo = None
+
+
+def make_communicator(group=None) -> Communicator:
+    """Build the Communicator over ``group`` (default: WORLD)."""
+    if not runtime_initialized():
+        raise IGGError("The distributed runtime has not been initialized.")
+    group = dist.GroupMember.WORLD if group is None else group
+    size = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if dist.get_backend(group) == "gloo":
+        gloo = group
+    else:
+        ranks = dist.get_process_group_ranks(group)
+        gloo = dist.new_group(ranks=ranks, backend="gloo")
+    c = Communicator(group=group, gloo=gloo, rank=rank, size=size)
+    c.local_rank, c.local_size = _local_rank(c)
+    return c
+
+
+def _local_rank(c: Communicator) -> tuple[int, int]:
+    """Node-local rank/size (MPI.Comm_split_type(COMM_TYPE_SHARED) equivalent)."""
+    lr, ls = os.environ.get("LOCAL_RANK"), os.environ.get("LOCAL_WORLD_SIZE")
+    if lr is not None and ls is not None and c.gloo == dist.GroupMember.WORLD:
+        return int(lr), int(ls)
+    host = socket.gethostname()
+    hosts = c.all_gather_object(host)
+    same = [r for r, h in enumerate(hosts) if h == host]
+    return same.index(c.rank), len(same)

@@ -1,0 +1,115 @@
+"""``gather_`` — assemble the global array on a root rank.
+
+Reference: ``gather!(A, A_global; root=0)`` (src/gather.jl:25-65). The block of
+the process with Cartesian coords (cx,cy,cz) lands at
+``A_global[cx*nx:(cx+1)*nx, cy*ny:..., cz*nz:...]``; only
+``A_global.numel() == nprocs*A.numel()`` is required (a 1-D ``A`` may be
+gathered into a 3-D ``A_global``); ``A_global`` may be ``None`` off-root; the
+root keeps a grow-only internal buffer until ``finalize_global_grid``.
+
+MI355X path: GPU ``A`` -> one RCCL group of receives on the root straight into
+a grow-only device buffer + a HIP reorder kernel (csrc/gather.cpp). CPU ``A``
+-> gloo point-to-point into a grow-only host buffer + one strided reorder copy.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .._native import ALLOC_GRANULARITY, IGGError, native
+from . import grid as _grid
+from .halo import field_tuple
+
+_host_buf = None  # grow-only flat uint8 host buffer
+_gatherer = None  # native device gatherer (grow-only device buffer)
+
+
+def free_gather_buffer() -> None:
+    global _host_buf, _gatherer
+    _host_buf = None
+    if _gatherer is not None:
+        _gatherer.free()
+    _gatherer = None
+
+
+def _padded_shape(A: torch.Tensor) -> list[int]:
+    return list(A.shape) + [1] * (3 - A.dim())
+
+
+def _global_view(A_global: torch.Tensor, s, dims) -> torch.Tensor:
+    shape = [int(dims[d]) * s[d] for d in range(3)]
+    if not A_global.is_contiguous():
+        raise IGGError("The input argument A_global must be a contiguous array.")
+    return A_global.view(shape)
+
+
+def gather_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) -> None:
+    """Gather ``A`` from every process into ``A_global`` on ``root``."""
+    gg = _grid.global_grid()
+    c = gg.comm
+    nprocs = int(gg.nprocs)
+    dims = [int(d) for d in gg.dims]
+    me = int(gg.me)
+    if me == root:
+        if A_global is None:
+            raise IGGError("The input argument A_global can't be `nothing` on the root")
+        if A_global.numel() != nprocs * A.numel():
+            raise IGGError("The input argument A_global must be of length nprocs*length(A)")
+        if A_global.dtype != A.dtype:
+            raise IGGError("The input arguments A and A_global must have the same element type.")
+    s = _padded_shape(A)
+    if A.is_cuda and nprocs > 1 and c.rccl is None and gg.amdgpu_enabled:
+        c.ensure_rccl()
+    if A.is_cuda and (nprocs == 1 or c.rccl is not None):
+        _gather_device(A, A_global, root, s, dims, me, nprocs, c)
+    else:
+        _gather_host(A.cpu() if A.is_cuda else A, A_global, root, s, dims, me, nprocs, c)
+
+
+def _gather_device(A, A_global, root, s, dims, me, nprocs, c) -> None:
+    global _gatherer
+    A = A.contiguous()
+    stream = torch.cuda.current_stream().cuda_stream
+    dst = None
+    if me == root:
+        dst = A_global if (A_global.is_cuda and A_global.is_contiguous()) else torch.empty(
+            A_global.shape, dtype=A.dtype, device=A.device)
+        _global_view(dst, s, dims)  # validates the shape
+    if nprocs == 1:
+        _global_view(dst, s, dims).copy_(A.view(s))
+    else:
+        if _gatherer is None:
+            _gatherer = native.Gatherer()
+        _gatherer.gather(field_tuple(A), dst.data_ptr() if dst is not None else 0, root, dims, c.rccl, stream)
+    if me == root and dst is not A_global:
+        A_global.copy_(dst)
+
+
+def _gather_host(A, A_global, root, s, dims, me, nprocs, c) -> None:
+    global _host_buf
+    A = A.contiguous()
+    nbytes = A.numel() * A.element_size()
+    if me != root:
+        dist.send(A.view(-1).view(torch.uint8), dst=c.global_rank(root), group=c.gloo)
+        return
+    need = -(-nprocs * A.numel() // ALLOC_GRANULARITY) * ALLOC_GRANULARITY * A.element_size()
+    if _host_buf is None or _host_buf.numel() < need:
+        _host_buf = None
+        _host_buf = torch.empty(need, dtype=torch.uint8)
+    flat = _host_buf[: nprocs * nbytes]
+    reqs = []
+    for p in range(nprocs):
+        if p != root:
+            reqs.append(dist.irecv(flat[p * nbytes:(p + 1) * nbytes], src=c.global_rank(p), group=c.gloo))
+    flat[root * nbytes:(root + 1) * nbytes].copy_(A.view(-1).view(torch.uint8))
+    for r in reqs:
+        r.wait()
+    blocks = flat.view(A.dtype).view(dims[0], dims[1], dims[2], s[0], s[1], s[2])
+    glob = blocks.permute(0, 3, 1, 4, 2, 5).reshape(dims[0] * s[0], dims[1] * s[1], dims[2] * s[2])
+    if A_global.is_contiguous() and A_global.device.type == "cpu":
+        _global_view(A_global, s, dims).copy_(glob)
+    else:
+        A_global.copy_(glob.reshape(A_global.shape).to(A_global.device))
+
+
+gather = gather_

@@ -1,0 +1,285 @@
+"""``update_halo_`` — halo update of one or more fields (CPU or GPU tensors).
+
+Reference: ``update_halo!`` (src/update_halo.jl:25-78) with its argument checks
+(:804-834), ranges (:544-563) and buffer pool (:92-339). The data path is the
+native C++ ``HaloEngine`` (csrc/halo.cpp): per dimension x -> y -> z, ONE fused
+pack launch for every face of every field, ONE RCCL group (device) or gloo
+phase (host), ONE fused unpack launch; contiguous faces go zero-copy; the
+periodic single-process case is one in-place copy launch. All GPU work is
+enqueued on the caller's current HIP stream with no host synchronisation.
+
+Layout: a field's logical axes (0, 1, 2) are the grid's (x, y, z); any dense
+memory layout works (the engine reads strides). PyTorch's default C order makes
+z contiguous, so the x-face is the zero-copy one and the z-face the strided one.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .._native import NDIMS, NNEIGHBORS, PROC_NULL, IGGError, native
+from ..utils import config
+from . import grid as _grid
+
+_engine = None
+_plans: dict = {}
+_MAX_PLANS = 512
+_buf_dtype = {False: None, True: None}
+_debug_sync = False
+
+
+def _join(items) -> str:
+    """Julia's ``join(v, ", ", " and ")``."""
+    s = [str(x) for x in items]
+    if len(s) <= 1:
+        return "".join(s)
+    return ", ".join(s[:-1]) + " and " + s[-1]
+
+
+def _jl_vec(v) -> str:
+    return "[" + ", ".join(str(x) for x in v) + "]"
+
+
+def _is_dense(t: torch.Tensor) -> bool:
+    if t.numel() <= 1:
+        return True
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz > 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
+def field_tuple(t: torch.Tensor):
+    """(ptr, ndims, size3, stride3, elem_bytes, device) for the native engine."""
+    nd = t.dim()
+    if nd < 1 or nd > NDIMS:
+        raise IGGError(f"Fields must have 1 to {NDIMS} dimensions (got {nd}).")
+    size = list(t.shape) + [1] * (NDIMS - nd)
+    stride = list(t.stride()) + [t.numel()] * (NDIMS - nd)
+    return (t.data_ptr(), nd, size, stride, t.element_size(), bool(t.is_cuda))
+
+
+def _grid_info(gg) -> "native.GridInfo":
+    return native.GridInfo(int(gg.me), int(gg.nprocs), gg.nxyz.tolist(), gg.overlaps.tolist(), gg.neighbors.tolist())
+
+
+def _init_engine(gg) -> None:
+    global _engine, _debug_sync
+    _plans.clear()
+    _engine = native.HaloEngine(_grid_info(gg))
+    _debug_sync = config.debug_sync()
+    if gg.nprocs > 1:
+        _engine.set_transport(gg.comm.host_transport(), False)
+        if gg.amdgpu_enabled:
+            _engine.set_transport(gg.comm.device_transport(), True)
+
+
+def _drop_engine() -> None:
+    global _engine
+    _plans.clear()
+    if _engine is not None:
+        _engine.pool_free()
+    _engine = None
+
+
+def engine():
+    _grid.check_initialized()
+    return _engine
+
+
+def sync_grid() -> None:
+    """Push the (possibly test-mutated) grid topology into the native engine."""
+    _plans.clear()
+    _engine.set_grid(_grid_info(_grid.global_grid()))
+
+
+# --- argument checks (update_halo.jl:804-834) ---------------------------------
+def _ol(gg, dim0: int, t: torch.Tensor) -> int:
+    s = int(t.shape[dim0]) if t.dim() > dim0 else 1
+    return int(gg.overlaps[dim0]) + s - int(gg.nxyz[dim0])
+
+
+def check_fields(*fields) -> None:
+    gg = _grid.global_grid()
+    for i, A in enumerate(fields):
+        if not isinstance(A, torch.Tensor):
+            raise IGGError(f"The field at position {i + 1} is not a torch.Tensor.")
+    no_halo = [i + 1 for i, A in enumerate(fields) if all(_ol(gg, d, A) < 2 for d in range(A.dim()))]
+    if len(no_halo) > 1:
+        raise IGGError(f"The fields at positions {_join(no_halo)} have no halo; remove them from the call.")
+    if len(no_halo) > 0:
+        raise IGGError(f"The field at position {no_halo[0]} has no halo; remove it from the call.")
+    dups = [
+        [i + 1, j + 1]
+        for i in range(len(fields))
+        for j in range(i + 1, len(fields))
+        if fields[i].device == fields[j].device and fields[i].data_ptr() == fields[j].data_ptr()
+    ]
+    if len(dups) > 2:
+        raise IGGError(
+            f"The pairs of fields with the positions {_join(_jl_vec(d) for d in dups)} are the same; "
+            "remove any duplicates from the call."
+        )
+    if len(dups) > 0:
+        raise IGGError(
+            f"The field at position {dups[0][1]} is a duplicate of the one at the position {dups[0][0]}; "
+            "remove the duplicate from the call."
+        )
+
+    def typ(A):
+        return (A.dtype, A.dim(), A.device.type)
+
+    diff = [i + 1 for i in range(1, len(fields)) if typ(fields[i]) != typ(fields[0])]
+    if len(diff) > 1:
+        raise IGGError(
+            f"The fields at positions {_join(diff)} are of different type than the first field; "
+            "make sure that in a same call all fields are of the same type."
+        )
+    if len(diff) == 1:
+        raise IGGError(
+            f"The field at position {diff[0]} is of different type than the first field; "
+            "make sure that in a same call all fields are of the same type."
+        )
+    for i, A in enumerate(fields):
+        if not _is_dense(A):
+            raise IGGError(
+                f"The field at position {i + 1} is not a dense array (a strided view); pass the full array."
+            )
+
+
+def _plan(fields):
+    key = tuple((A.data_ptr(), A.shape, A.stride(), A.dtype, A.device) for A in fields)
+    p = _plans.get(key)
+    if p is None:
+        check_fields(*fields)
+        gg = _grid.global_grid()
+        device = fields[0].is_cuda
+        if device and not gg.amdgpu_enabled:
+            raise IGGError(
+                "AMDGPU is not enabled (possibly detected non functional when the ImplicitGlobalGrid module was loaded)."
+            )
+        if len(_plans) >= _MAX_PLANS:
+            _plans.clear()
+        p = (native.FieldSet([field_tuple(A) for A in fields]), device, fields[0].dtype)
+        _plans[key] = p
+    return p
+
+
+def update_halo_(*fields) -> None:
+    """Update the halo of the given field(s) (``update_halo!``).
+
+    Group fields in one call for better performance: every dimension then needs
+    one pack launch, one communication phase and one unpack launch for all of
+    them. GPU work is stream-ordered on ``torch.cuda.current_stream()``.
+    """
+    _grid.check_initialized()
+    if not fields:
+        return
+    fs, device, dtype = _plan(fields)
+    stream = torch.cuda.current_stream().cuda_stream if device else 0
+    _engine.exchange_set(fs, stream)
+    _buf_dtype[device] = dtype
+    if _debug_sync and device:
+        native.stream_synchronize(stream)
+
+
+update_halo = update_halo_
+
+
+# --- ranges (update_halo.jl:544-563), 1-based like the reference --------------
+def sendranges(n: int, dim: int, A: torch.Tensor) -> list[range]:
+    gg = _grid.global_grid()
+    o = _ol(gg, dim - 1, A)
+    if o < 2:
+        raise IGGError("Incoherent arguments: ol(A,dim)<2.")
+    size = [int(A.shape[d]) if A.dim() > d else 1 for d in range(NDIMS)]
+    i = size[dim - 1] - (o - 1) if n == 2 else 1 + (o - 1)
+    r = [range(1, s + 1) for s in size]
+    r[dim - 1] = range(i, i + 1)
+    return r
+
+
+def recvranges(n: int, dim: int, A: torch.Tensor) -> list[range]:
+    gg = _grid.global_grid()
+    if _ol(gg, dim - 1, A) < 2:
+        raise IGGError("Incoherent arguments: ol(A,dim)<2.")
+    size = [int(A.shape[d]) if A.dim() > d else 1 for d in range(NDIMS)]
+    i = size[dim - 1] if n == 2 else 1
+    r = [range(1, s + 1) for s in size]
+    r[dim - 1] = range(i, i + 1)
+    return r
+
+
+def halosize(dim: int, A: torch.Tensor) -> tuple:
+    """Shape of the halo of ``A`` in ``dim`` (update_halo.jl:84)."""
+    if A.dim() > 1:
+        return tuple(int(s) for d, s in enumerate(A.shape) if d != dim - 1)
+    return (1,)
+
+
+# --- buffer pool hooks (update_halo.jl:104-187, 332-338) ------------------------
+def allocate_bufs(*fields) -> None:
+    _grid.check_initialized()
+    device = fields[0].is_cuda
+    _engine.pool_ensure([field_tuple(A) for A in fields], device)
+    _buf_dtype[device] = fields[0].dtype
+
+
+def free_update_halo_buffers() -> None:
+    if _engine is not None:
+        native.device_synchronize() if _engine.pool_allocated(True) else None
+        _engine.pool_free()
+    _buf_dtype[False] = _buf_dtype[True] = None
+
+
+def _bufs(which: int, device: bool):
+    if _engine is None or not _engine.pool_allocated(device):
+        return None
+    dtype = _buf_dtype[device] or torch.float64
+    esize = torch.empty(0, dtype=dtype).element_size()
+    out = []
+    from .comm import _device_view, _host_view
+
+    for slot in range(_engine.pool_nslots(device)):
+        ptrs = _engine.pool_ptrs(slot, device)
+        cap = _engine.pool_capacity(slot, device)
+        pair = []
+        for n in range(NNEIGHBORS):
+            ptr = ptrs[which * 2 + n]
+            raw = _device_view(ptr, cap) if device else _host_view(ptr, cap)
+            pair.append(raw[: (cap // esize) * esize].view(dtype))
+        out.append(pair)
+    return out
+
+
+def get_sendbufs_raw(device: bool = False):
+    """Views of the send buffers (list per field slot of [left, right]); None if freed."""
+    return _bufs(0, device)
+
+
+def get_recvbufs_raw(device: bool = False):
+    return _bufs(1, device)
+
+
+def halo_plan_summary(*fields) -> list[dict]:
+    """Describe what an exchange of ``fields`` does per dim (debug/profiling aid)."""
+    gg = _grid.global_grid()
+    out = []
+    for d in range(NDIMS):
+        nb = gg.neighbors[:, d]
+        entry = {"dim": d + 1, "neighbors": nb.tolist(), "faces": []}
+        for i, A in enumerate(fields):
+            if _ol(gg, d, A) < 2:
+                continue
+            ft = field_tuple(A)
+            for s in range(NNEIGHBORS):
+                if nb[s] == PROC_NULL:
+                    continue
+                idx = native.send_index(_engine.grid, s, d, ft)
+                info = native.face_info(ft, d, idx)
+                entry["faces"].append({"field": i + 1, "side": s + 1, "bytes": info[6], "zero_copy": bool(info[5])})
+        out.append(entry)
+    return out

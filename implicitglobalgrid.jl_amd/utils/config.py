@@ -1,0 +1,69 @@
+"""Configuration from environment variables.
+
+Reference flags (src/init_global_grid.jl:51-68, module docs
+src/ImplicitGlobalGrid.jl:26-33) are parsed with the reference's precedence
+rules and stored on the grid:
+
+* ``IGG_ROCMAWARE_MPI`` / ``IGG_CUDAAWARE_MPI`` set all three dims; the per-dim
+  ``*_DIMX/_DIMY/_DIMZ`` variants are only honoured if the global variable left
+  every dim false.
+* ``IGG_LOOPVECTORIZATION`` sets all dims; per-dim variants are only honoured if
+  the global variable set every dim true (they can only *disable* dims).
+
+On MI355X device data always moves device-resident (RCCL), so the "aware" flags
+are informational; ``loopvectorization[d]`` selects the threaded host copy for
+CPU fields in dim ``d`` (default: on).
+
+Framework knobs (new): ``IGG_TRANSPORT`` (``rccl`` | ``torch``) for GPU
+point-to-point, ``IGG_STENCIL_VARIANT`` (int or ``auto``), ``IGG_DEBUG_SYNC``
+(synchronise after every halo update), ``IGG_QUIET``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Mapping
+
+
+def _flag(env: Mapping[str, str], key: str) -> bool:
+    return int(env[key]) > 0
+
+
+def parse_aware_flags(prefix: str, env: Mapping[str, str] | None = None) -> list[bool]:
+    """``IGG_<prefix>`` then per-dim overrides if the global left all dims false."""
+    env = os.environ if env is None else env
+    flags = [False, False, False]
+    if f"IGG_{prefix}" in env:
+        flags = [_flag(env, f"IGG_{prefix}")] * 3
+    if not any(flags):
+        for d, ax in enumerate("XYZ"):
+            k = f"IGG_{prefix}_DIM{ax}"
+            if k in env:
+                flags[d] = _flag(env, k)
+    return list(flags)
+
+
+def parse_loopvectorization(env: Mapping[str, str] | None = None) -> list[bool]:
+    """``IGG_LOOPVECTORIZATION``; per-dim variables only honoured if all dims true."""
+    env = os.environ if env is None else env
+    flags = [False, False, False]
+    if "IGG_LOOPVECTORIZATION" in env:
+        flags = [_flag(env, "IGG_LOOPVECTORIZATION")] * 3
+    if all(flags):
+        for d, ax in enumerate("XYZ"):
+            k = f"IGG_LOOPVECTORIZATION_DIM{ax}"
+            if k in env:
+                flags[d] = _flag(env, k)
+    return list(flags)
+
+
+def transport_choice(env: Mapping[str, str] | None = None) -> str:
+    env = os.environ if env is None else env
+    t = env.get("IGG_TRANSPORT", "rccl").strip().lower()
+    if t not in ("rccl", "torch"):
+        raise ValueError(f"IGG_TRANSPORT must be 'rccl' or 'torch' (got {t!r})")
+    return t
+
+
+def debug_sync(env: Mapping[str, str] | None = None) -> bool:
+    env = os.environ if env is None else env
+    return env.get("IGG_DEBUG_SYNC", "0") not in ("", "0")
