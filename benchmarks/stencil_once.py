@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Run selected stencil variants a few times on n^3 (for rocprofv3 counters)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import igg  # noqa: E402
+from igg._native import native  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=512)
+ap.add_argument("--variants", default="0")
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--dtype", default="float64")
+a = ap.parse_args()
+dt = getattr(torch, a.dtype)
+n = a.n
+T = torch.rand((n, n, n), dtype=dt, device="cuda")
+Cp = 1 + torch.rand((n, n, n), dtype=dt, device="cuda")
+T2 = T.clone()
+s = torch.cuda.current_stream().cuda_stream
+for v in [int(x) for x in a.variants.split(",")]:
+    for _ in range(a.reps):
+        native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], [1.0, 1.0, 1.0], 0.01,
+                           T.element_size(), [((1, 1, 1), (n - 1, n - 1, n - 1))], True, v, s)
+torch.cuda.synchronize()
+print("done")

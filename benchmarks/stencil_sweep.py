@@ -30,7 +30,7 @@ def run(v, T2, T, Cp, boxes, rd2, dtlam, stream):
 def correctness(dtype):
     g = torch.Generator().manual_seed(0)
     worst = {}
-    for shape in [(17, 13, 70), (40, 33, 129), (9, 70, 67)]:
+    for shape in [(17, 13, 70), (40, 33, 129), (9, 70, 68), (12, 9, 132), (6, 5, 256), (5, 130, 512)]:
         T = torch.rand(shape, generator=g, dtype=dtype)
         Cp = 1 + torch.rand(shape, generator=g, dtype=dtype)
         boxes_list = [[((1, 1, 1), tuple(s - 1 for s in shape))],
@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--dtype", default="float64")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--grid-rounds", default="1,2,0", help="residency rounds per launch to sweep")
+    ap.add_argument("--variants", default="all")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     dtype = getattr(torch, a.dtype)
@@ -65,19 +67,23 @@ def main():
     T2 = T.clone()
     boxes = [((1, 1, 1), (n - 1, n - 1, n - 1))]
     s = torch.cuda.current_stream()
-    times = {v: [] for v in range(len(names))}
-    for v in times:
+    vs = range(len(names)) if a.variants == "all" else [int(x) for x in a.variants.split(",")]
+    grs = [int(x) for x in a.grid_rounds.split(",")]
+    times = {(g, v): [] for g in grs for v in vs}
+    for g, v in times:
+        native.diffusion3d_set_rounds(g)
         run(v, T2, T, Cp, boxes, [1.0, 1.0, 1.0], 0.01, s.cuda_stream)
     ref_out = None
     for r in range(a.rounds):
-        for v in times:
+        for g, v in times:
+            native.diffusion3d_set_rounds(g)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(a.reps):
                 run(v, T2, T, Cp, boxes, [1.0, 1.0, 1.0], 0.01, s.cuda_stream)
             e1.record(s)
             e1.synchronize()
-            times[v].append(e0.elapsed_time(e1) / a.reps)
+            times[(g, v)].append(e0.elapsed_time(e1) / a.reps)
             if r == 0:
                 if ref_out is None:
                     ref_out = T2.clone()
@@ -85,9 +91,9 @@ def main():
                     print(f"variant {names[v]} differs from variant 0: {(T2-ref_out).abs().max().item()}")
     abytes = 3 * n ** 3 * T.element_size()
     res = {}
-    for v, ts in times.items():
+    for (g, v), ts in sorted(times.items(), key=lambda kv: statistics.median(kv[1])):
         med, mn = statistics.median(ts), min(ts)
-        res[names[v]] = {"ms_median": round(med, 4), "ms_min": round(mn, 4), "T_eff_GBs": round(abytes / (med * 1e-3) / 1e9, 1)}
+        res[f"{names[v]}@r{g}"] = {"ms_median": round(med, 4), "ms_min": round(mn, 4), "T_eff_GBs": round(abytes / (med * 1e-3) / 1e9, 1)}
     # roofline: device copy
     x = torch.empty(2 ** 31 // 8, dtype=torch.float64, device="cuda")
     y = torch.empty_like(x)

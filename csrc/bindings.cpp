@@ -16,6 +16,11 @@
 #include "igg/stencil.hpp"
 #include "igg/topology.hpp"
 
+namespace igg {
+void launch_stream_probe(int kind, double* out, const double* a, const double* b, int64_t n, int blocks,
+                         hipStream_t stream);
+}
+
 namespace py = pybind11;
 using namespace igg;
 
@@ -284,6 +289,13 @@ PYBIND11_MODULE(_igg_native, m) {
     for (int i = 0; i < diffusion3d_num_variants(); ++i) v.push_back(diffusion3d_variant_name(i));
     return v;
   });
+  m.def("stream_probe", [](int kind, uintptr_t out, uintptr_t a, uintptr_t b, int64_t n, int blocks,
+                           uintptr_t stream) {
+    launch_stream_probe(kind, reinterpret_cast<double*>(out), reinterpret_cast<const double*>(a),
+                        reinterpret_cast<const double*>(b), n, blocks, as_stream(stream));
+  });
+  m.def("diffusion3d_set_rounds", &diffusion3d_set_rounds);
+  m.def("diffusion3d_get_rounds", &diffusion3d_get_rounds);
   m.def("diffusion3d",
         [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
            double dtlam, int elem_bytes, const std::vector<std::pair<Int3, Int3>>& boxes,

@@ -35,6 +35,9 @@ struct DiffusionArgs {
 // Number of tuned kernel variants (see stencil_kernels.hip); variant 0 = default.
 int diffusion3d_num_variants();
 const char* diffusion3d_variant_name(int v);
+// Grid sizing: number of full residency rounds per launch (<= 0: fixed 4096-block target).
+void diffusion3d_set_rounds(int rounds);
+int diffusion3d_get_rounds();
 
 void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, int variant,
                         hipStream_t stream);

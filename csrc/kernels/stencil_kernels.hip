@@ -28,6 +28,7 @@ struct BoxTable {
   int64_t lo[MAX_BOXES][3];
   int64_t hi[MAX_BOXES][3];
   int64_t ntz[MAX_BOXES], nty[MAX_BOXES], ch[MAX_BOXES];
+  int64_t zt0[MAX_BOXES];  // first z tile origin (vector kernel: aligned to 64*VZ)
   int64_t start[MAX_BOXES + 1];
   int n;
 };
@@ -125,72 +126,283 @@ diffusion3d_kernel(const KArgs<T> a, const BoxTable bt) {
   }
 }
 
-struct Variant {
-  const char* name;
-  int by, ry;
-  bool xcd;
+// Vectorised variant: each lane owns VZ consecutive z points (16 B per lane for
+// f64 VZ=2), so one wave covers a 64*VZ-point (1 KiB) contiguous row segment
+// with one global_load_dwordx4 per array. Tiles are aligned to row starts, so
+// every vector access is naturally aligned (requires n2 % VZ == 0). The z
+// neighbours come from the lane's own vector and its two lane neighbours
+// (__shfl up/down = ds_bpermute); only the two tile-edge values are loaded
+// (wave-uniform address). Row bases are wave-uniform (readfirstlane) so the
+// per-lane address is a 32-bit offset. PF: prefetch plane x+2 of T and x+1 of
+// Cp while computing plane x. NT: non-temporal stores of T2 (streamed once).
+template <typename T, int VZ>
+struct VecOf {
+  typedef T type __attribute__((ext_vector_type(VZ)));
 };
 
-// Keep in sync with dispatch() below.
+template <typename T, int VZ>
+__device__ __forceinline__ typename VecOf<T, VZ>::type vload(const T* p) {
+  return *reinterpret_cast<const typename VecOf<T, VZ>::type*>(p);
+}
+
+template <typename T, int BY, int RY, int VZ, bool PF, bool NT, int BZ>
+__global__ void __launch_bounds__(64 * BY * BZ)
+diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
+  using V = typename VecOf<T, VZ>::type;
+  constexpr int W = 64 * VZ * BZ;  // block tile width along z
+  const int64_t nb = bt.start[bt.n];
+  const int64_t b = xcd_remap(blockIdx.x, nb);
+  int k = 0;
+  while (k + 1 < bt.n && b >= bt.start[k + 1]) ++k;
+  int64_t local = b - bt.start[k];
+  const int64_t tz = local % bt.ntz[k];
+  local /= bt.ntz[k];
+  const int64_t ty = local % bt.nty[k];
+  const int64_t cx = local / bt.nty[k];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wz = wid % BZ, wy = wid / BZ;
+  const int64_t zt = bt.zt0[k] + tz * W + wz * (64 * VZ);    // wave-uniform segment origin
+  const int64_t y0 = bt.lo[k][1] + ty * (BY * RY) + wy * RY;
+  const int64_t xs = bt.lo[k][0] + cx * bt.ch[k];
+  const int64_t xe = min(xs + bt.ch[k], bt.hi[k][0]);
+  const int nv = static_cast<int>(min<int64_t>(RY, bt.hi[k][1] - y0));
+  if (nv <= 0) return;
+  const int64_t lo2 = bt.lo[k][2], hi2 = bt.hi[k][2];
+  const int64_t n2 = a.n2, s1 = a.n2, s0 = a.n1 * a.n2;
+  const int64_t z0 = zt + lane * VZ;
+  const int zl = static_cast<int>(min(z0, n2 - VZ) - zt);    // per-lane offset in the tile
+  const bool lane_full = z0 >= lo2 && z0 + VZ <= hi2;
+  if (zt >= hi2) return;  // whole wave segment past the box (partial last tile)
+  const int64_t zem = max<int64_t>(zt - 1, 0) - zt, zep = min<int64_t>(zt + 64 * VZ, n2 - 1) - zt;
+
+  int64_t rowb[RY];  // wave-uniform row bases (element index of the tile origin)
+#pragma unroll
+  for (int r = 0; r < RY; ++r) rowb[r] = (y0 + min(r, nv - 1)) * s1 + zt;
+  const int64_t rowm = (y0 - 1) * s1 + zt, rowp = (y0 + nv) * s1 + zt;
+
+  const T* __restrict__ t = a.t;
+  const T* __restrict__ cpp = a.cp;
+  V tm[RY], tc[RY], tp[RY], cp[RY];
+#pragma unroll
+  for (int r = 0; r < RY; ++r) {
+    tm[r] = vload<T, VZ>(t + (xs - 1) * s0 + rowb[r] + zl);
+    tc[r] = vload<T, VZ>(t + xs * s0 + rowb[r] + zl);
+    tp[r] = vload<T, VZ>(t + (xs + 1) * s0 + rowb[r] + zl);
+    cp[r] = vload<T, VZ>(cpp + xs * s0 + rowb[r] + zl);
+  }
+  const T two = T(2);
+  for (int64_t x = xs; x < xe; ++x) {
+    const int64_t off = x * s0;
+    V tn[RY], cpn[RY];
+    if (PF) {
+      const int64_t xn = min(x + 2, a.n0 - 1), xc = min(x + 1, xe - 1);
+#pragma unroll
+      for (int r = 0; r < RY; ++r) {
+        tn[r] = vload<T, VZ>(t + xn * s0 + rowb[r] + zl);
+        cpn[r] = vload<T, VZ>(cpp + xc * s0 + rowb[r] + zl);
+      }
+    }
+    const V ym = vload<T, VZ>(t + off + rowm + zl);
+    const V yp = vload<T, VZ>(t + off + rowp + zl);
+    T em[RY], ep[RY];
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      em[r] = t[off + rowb[r] + zem];
+      ep[r] = t[off + rowb[r] + zep];
+    }
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      const V& c = tc[r];
+      const V& yv = (r == 0) ? ym : tc[r > 0 ? r - 1 : 0];
+      const V& yn = (r + 1 < nv) ? tc[(r + 1 < RY) ? r + 1 : r] : yp;
+      T prev = __shfl_up(c[VZ - 1], 1);
+      T next = __shfl_down(c[0], 1);
+      if (lane == 0) prev = em[r];
+      if (lane == 63) next = ep[r];
+      V out;
+#pragma unroll
+      for (int e = 0; e < VZ; ++e) {
+        const T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
+        const T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
+        const T c2 = two * c[e];
+        const T lap = (tp[r][e] - c2 + tm[r][e]) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
+                      (zp - c2 + zm) * a.rdz2;
+        out[e] = c[e] + a.dtlam / cp[r][e] * lap;
+      }
+      if (r < nv) {
+        T* dst = a.t2 + off + rowb[r] + zl;
+        if (lane_full) {
+          if (NT) __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
+          else *reinterpret_cast<V*>(dst) = out;
+        } else {
+#pragma unroll
+          for (int e = 0; e < VZ; ++e)
+            if (z0 + e >= lo2 && z0 + e < hi2 && zt + zl == z0) dst[e] = out[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      tm[r] = tc[r];
+      tc[r] = tp[r];
+      if (PF) {
+        tp[r] = tn[r];
+        cp[r] = cpn[r];
+      }
+    }
+    if (!PF && x + 1 < xe) {
+#pragma unroll
+      for (int r = 0; r < RY; ++r) {
+        tp[r] = vload<T, VZ>(t + (x + 2) * s0 + rowb[r] + zl);
+        cp[r] = vload<T, VZ>(cpp + (x + 1) * s0 + rowb[r] + zl);
+      }
+    }
+  }
+}
+
+struct Variant {
+  const char* name;
+  int by, ry, vz;  // vz = 1: scalar kernel
+  bool pf, nt;
+};
+
+// Tuned variants; keep in sync with dispatch() below. Default (0) is the best
+// measured on MI355X for 512^3 f64 (benchmarks/stencil_sweep.py).
 constexpr Variant VARIANTS[] = {
-    {"by4_ry4_xcd", 4, 4, true},  {"by4_ry2_xcd", 4, 2, true}, {"by2_ry8_xcd", 2, 8, true},
-    {"by8_ry2_xcd", 8, 2, true},  {"by4_ry8_xcd", 4, 8, true}, {"by4_ry4_noxcd", 4, 4, false},
-    {"by1_ry16_xcd", 1, 16, true},
+    {"v4_by4_ry4_nt", 4, 4, 4, false, true},     // 0
+    {"s_by4_ry8", 4, 8, 1, false, false},        // 1 (scalar fallback family)
+    {"v2_by4_ry4_pf_nt", 4, 4, 2, true, true},   // 2
+    {"v4_by4_ry4", 4, 4, 4, false, false},       // 3
+    {"v4_by4_ry4_pf_nt", 4, 4, 4, true, true},   // 4
+    {"v4_by4_ry2_nt", 4, 2, 4, false, true},     // 5
+    {"v8_by4_ry2_nt", 4, 2, 8, false, true},     // 6
+    {"v4_by2_ry4_nt", 2, 4, 4, false, true},     // 7
+    {"v4_by8_ry2_nt", 8, 2, 4, false, true},     // 8
+    {"v4_by4_ry8_nt", 4, 8, 4, false, true},     // 9
+    {"v8_by2_ry2_nt", 2, 2, 8, false, true},     // 10
+    {"v2_by4_ry8_nt", 4, 8, 2, false, true},     // 11
+    {"v4_bz2_by8_ry4_nt", 8, 4, 4, false, true}, // 12 (1024-thread blocks)
+    {"v4_bz2_by4_ry4_nt", 4, 4, 4, false, true}, // 13
+    {"v4_bz2_by2_ry8_nt", 2, 8, 4, false, true}, // 14
+    {"v2_bz2_by4_ry8_nt", 4, 8, 2, false, true}, // 15
+    {"v4_bz2_by8_ry2_nt", 8, 2, 4, false, true}, // 16
+    {"v2_bz4_by4_ry4_nt", 4, 4, 2, false, true}, // 17
 };
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
-template <typename T, int BY, int RY, bool XCD>
-void launch_one(const KArgs<T>& ka, const std::vector<Box>& boxes, hipStream_t stream) {
-  constexpr int TY = BY * RY;
-  const int64_t target_blocks = 4096;
+// Grid sizing policy: `g_rounds` full residency rounds (resident workgroups =
+// occupancy x CUs); the x-march is chunked so every block gets equal work and
+// no partial last round leaves CUs idle. g_rounds <= 0: fixed 4096-block target.
+int g_rounds = 1;
+
+int resident_blocks(const void* kernel, int block) {
+  static std::vector<std::pair<const void*, int>> cache;
+  for (const auto& c : cache)
+    if (c.first == kernel) return c.second;
+  int dev = 0, cus = 0, occ = 0;
+  IGG_HIP_CHECK(hipGetDevice(&dev));
+  IGG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  IGG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, 0));
+  const int r = std::max(1, occ) * std::max(1, cus);
+  cache.emplace_back(kernel, r);
+  return r;
+}
+
+// Build the box tables (<= MAX_BOXES per launch) for tile width W (z) and
+// tile height TY (y); `aligned`: z tiles start at multiples of W.
+template <typename F>
+void for_each_table(const std::vector<Box>& boxes, int W, int TY, bool aligned, int64_t target_blocks,
+                    F&& launch) {
   size_t pos = 0;
   while (pos < boxes.size()) {
-    BoxTable bt{};
-    int64_t blocks = 0;
-    bt.n = 0;
-    // first pass: tile counts (for the chunk heuristic we need the total tiles)
     std::vector<Box> grp;
     while (pos < boxes.size() && static_cast<int>(grp.size()) < MAX_BOXES) {
       if (!boxes[pos].empty()) grp.push_back(boxes[pos]);
       ++pos;
     }
     if (grp.empty()) continue;
-    int64_t tiles = 0;
-    for (const Box& bx : grp)
-      tiles += ((bx.hi[2] - bx.lo[2] + 63) / 64) * ((bx.hi[1] - bx.lo[1] + TY - 1) / TY);
-    const int64_t chunks_wanted = std::max<int64_t>(1, (target_blocks + tiles - 1) / tiles);
+    BoxTable bt{};
+    bt.n = 0;
+    int64_t blocks = 0, tiles = 0, len_sum = 0;
+    auto zt0 = [&](const Box& bx) { return aligned ? (bx.lo[2] / W) * W : bx.lo[2]; };
+    for (const Box& bx : grp) {
+      const int64_t t = ((bx.hi[2] - zt0(bx) + W - 1) / W) * ((bx.hi[1] - bx.lo[1] + TY - 1) / TY);
+      tiles += t;
+      len_sum += t * (bx.hi[0] - bx.lo[0]);
+    }
+    // Planes per block so that sum(tiles * len0 / ch) ~= target_blocks.
+    int64_t ch_all = std::max<int64_t>(1, (len_sum + target_blocks - 1) / target_blocks);
     for (const Box& bx : grp) {
       const int k = bt.n++;
       for (int d = 0; d < 3; ++d) { bt.lo[k][d] = bx.lo[d]; bt.hi[k][d] = bx.hi[d]; }
       const int64_t len0 = bx.hi[0] - bx.lo[0];
-      bt.ntz[k] = (bx.hi[2] - bx.lo[2] + 63) / 64;
+      bt.zt0[k] = zt0(bx);
+      bt.ntz[k] = (bx.hi[2] - bt.zt0[k] + W - 1) / W;
       bt.nty[k] = (bx.hi[1] - bx.lo[1] + TY - 1) / TY;
-      // March length: long enough to amortise the 2-plane prologue, short
-      // enough to give ~target_blocks workgroups (>> 256 CUs).
-      int64_t ch = (len0 + chunks_wanted - 1) / chunks_wanted;
-      ch = std::max<int64_t>(ch, std::min<int64_t>(len0, 32));
+      // Equal-size chunks along the march (no short remainder chunk).
+      const int64_t nch = std::max<int64_t>(1, (len0 + ch_all - 1) / ch_all);
+      const int64_t ch = (len0 + nch - 1) / nch;
       bt.ch[k] = ch;
       bt.start[k] = blocks;
       blocks += bt.ntz[k] * bt.nty[k] * ((len0 + ch - 1) / ch);
     }
     bt.start[bt.n] = blocks;
     if (blocks > 0x7fffffffLL) fail("diffusion3d: grid too large");
-    hipLaunchKernelGGL((diffusion3d_kernel<T, BY, RY, XCD>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(64 * BY), 0, stream, ka, bt);
-    IGG_HIP_CHECK(hipGetLastError());
+    launch(bt, static_cast<unsigned>(blocks));
   }
+}
+
+int64_t target_for(const void* kernel, int block) {
+  if (g_rounds <= 0) return 4096;
+  return static_cast<int64_t>(g_rounds) * resident_blocks(kernel, block);
+}
+
+template <typename T, int BY, int RY, bool XCD>
+void launch_scalar(const KArgs<T>& ka, const std::vector<Box>& boxes, hipStream_t stream) {
+  const void* kern = reinterpret_cast<const void*>(&diffusion3d_kernel<T, BY, RY, XCD>);
+  for_each_table(boxes, 64, BY * RY, false, target_for(kern, 64 * BY), [&](const BoxTable& bt, unsigned blocks) {
+    hipLaunchKernelGGL((diffusion3d_kernel<T, BY, RY, XCD>), dim3(blocks), dim3(64 * BY), 0, stream, ka, bt);
+    IGG_HIP_CHECK(hipGetLastError());
+  });
+}
+
+template <typename T, int BY, int RY, int VZ, bool PF, bool NT, int BZ = 1>
+void launch_vector(const KArgs<T>& ka, const std::vector<Box>& boxes, hipStream_t stream) {
+  if (ka.n2 % VZ != 0 || ka.n2 < 2 * VZ) {  // vector path needs aligned rows
+    launch_scalar<T, 4, 8, true>(ka, boxes, stream);
+    return;
+  }
+  const void* kern = reinterpret_cast<const void*>(&diffusion3d_vkernel<T, BY, RY, VZ, PF, NT, BZ>);
+  for_each_table(boxes, 64 * VZ * BZ, BY * RY, true, target_for(kern, 64 * BY * BZ), [&](const BoxTable& bt, unsigned blocks) {
+    hipLaunchKernelGGL((diffusion3d_vkernel<T, BY, RY, VZ, PF, NT, BZ>), dim3(blocks), dim3(64 * BY * BZ), 0,
+                       stream, ka, bt);
+    IGG_HIP_CHECK(hipGetLastError());
+  });
 }
 
 template <typename T>
 void dispatch(const KArgs<T>& ka, const std::vector<Box>& boxes, int v, hipStream_t s) {
   switch (v) {
-    case 0: launch_one<T, 4, 4, true>(ka, boxes, s); break;
-    case 1: launch_one<T, 4, 2, true>(ka, boxes, s); break;
-    case 2: launch_one<T, 2, 8, true>(ka, boxes, s); break;
-    case 3: launch_one<T, 8, 2, true>(ka, boxes, s); break;
-    case 4: launch_one<T, 4, 8, true>(ka, boxes, s); break;
-    case 5: launch_one<T, 4, 4, false>(ka, boxes, s); break;
-    case 6: launch_one<T, 1, 16, true>(ka, boxes, s); break;
+    case 0: launch_vector<T, 4, 4, 4, false, true>(ka, boxes, s); break;
+    case 1: launch_scalar<T, 4, 8, true>(ka, boxes, s); break;
+    case 2: launch_vector<T, 4, 4, 2, true, true>(ka, boxes, s); break;
+    case 3: launch_vector<T, 4, 4, 4, false, false>(ka, boxes, s); break;
+    case 4: launch_vector<T, 4, 4, 4, true, true>(ka, boxes, s); break;
+    case 5: launch_vector<T, 4, 2, 4, false, true>(ka, boxes, s); break;
+    case 6: launch_vector<T, 4, 2, 8, false, true>(ka, boxes, s); break;
+    case 7: launch_vector<T, 2, 4, 4, false, true>(ka, boxes, s); break;
+    case 8: launch_vector<T, 8, 2, 4, false, true>(ka, boxes, s); break;
+    case 9: launch_vector<T, 4, 8, 4, false, true>(ka, boxes, s); break;
+    case 10: launch_vector<T, 2, 2, 8, false, true>(ka, boxes, s); break;
+    case 11: launch_vector<T, 4, 8, 2, false, true>(ka, boxes, s); break;
+    case 12: launch_vector<T, 8, 4, 4, false, true, 2>(ka, boxes, s); break;
+    case 13: launch_vector<T, 4, 4, 4, false, true, 2>(ka, boxes, s); break;
+    case 14: launch_vector<T, 2, 8, 4, false, true, 2>(ka, boxes, s); break;
+    case 15: launch_vector<T, 4, 8, 2, false, true, 2>(ka, boxes, s); break;
+    case 16: launch_vector<T, 8, 2, 4, false, true, 2>(ka, boxes, s); break;
+    case 17: launch_vector<T, 4, 4, 2, false, true, 4>(ka, boxes, s); break;
     default: fail("diffusion3d: invalid kernel variant ", v);
   }
 }
@@ -212,6 +424,8 @@ KArgs<T> make_args(const DiffusionArgs& a) {
 }  // namespace
 
 int diffusion3d_num_variants() { return NVARIANTS; }
+void diffusion3d_set_rounds(int rounds) { g_rounds = rounds; }
+int diffusion3d_get_rounds() { return g_rounds; }
 const char* diffusion3d_variant_name(int v) {
   return (v >= 0 && v < NVARIANTS) ? VARIANTS[v].name : "invalid";
 }

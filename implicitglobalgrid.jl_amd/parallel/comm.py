@@ -140,7 +140,14 @@ class Communicator:
     def device_transport(self):
         if self.size == 1:
             return None
-        if config.transport_choice() == "torch":
+        choice = config.transport_choice()
+        if choice == "staged":
+            t = self._transports.get("staged")
+            if t is None:
+                t = native.PyTransport(self._staged_p2p, False, True, "gloo-staged")
+                self._transports["staged"] = t
+            return t
+        if choice == "torch":
             t = self._transports.get("torch")
             if t is None:
                 self._ensure_torch_nccl()
@@ -172,6 +179,21 @@ class Communicator:
             reqs.append(dist.isend(_host_view(ptr, nbytes), dst=self.global_rank(peer), group=self.gloo, tag=tag))
         for r in reqs:
             r.wait()
+
+    def _staged_p2p(self, recvs, sends, device, stream):
+        """Host-staged device exchange (the reference's non-GPU-aware MPI path,
+        update_halo.jl:437,465): D2H of the send buffers, gloo, H2D."""
+        s = torch.cuda.ExternalStream(stream)
+        with torch.cuda.stream(s):
+            hs = [(_device_view(p, n).cpu(), peer, tag) for p, n, peer, tag in sends]
+            hr = [(torch.empty(n, dtype=torch.uint8), p, peer, tag) for p, n, peer, tag in recvs]
+        reqs = [dist.irecv(h, src=self.global_rank(peer), group=self.gloo, tag=tag) for h, _p, peer, tag in hr]
+        reqs += [dist.isend(h, dst=self.global_rank(peer), group=self.gloo, tag=tag) for h, peer, tag in hs]
+        for r in reqs:
+            r.wait()
+        with torch.cuda.stream(s):
+            for h, p, _peer, _tag in hr:
+                _device_view(p, h.numel()).copy_(h, non_blocking=False)
 
     def _torch_p2p(self, recvs, sends, device, stream):
         ops = []

@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 
 from .._native import ALLOC_GRANULARITY, IGGError, native
+from ..utils import config
 from . import grid as _grid
 from .halo import field_tuple
 
@@ -58,7 +59,7 @@ def gather_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) ->
         if A_global.dtype != A.dtype:
             raise IGGError("The input arguments A and A_global must have the same element type.")
     s = _padded_shape(A)
-    if A.is_cuda and nprocs > 1 and c.rccl is None and gg.amdgpu_enabled:
+    if A.is_cuda and nprocs > 1 and c.rccl is None and gg.amdgpu_enabled and config.transport_choice() == "rccl":
         c.ensure_rccl()
     if A.is_cuda and (nprocs == 1 or c.rccl is not None):
         _gather_device(A, A_global, root, s, dims, me, nprocs, c)

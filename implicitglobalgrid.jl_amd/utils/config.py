@@ -14,8 +14,9 @@ On MI355X device data always moves device-resident (RCCL), so the "aware" flags
 are informational; ``loopvectorization[d]`` selects the threaded host copy for
 CPU fields in dim ``d`` (default: on).
 
-Framework knobs (new): ``IGG_TRANSPORT`` (``rccl`` | ``torch``) for GPU
-point-to-point, ``IGG_STENCIL_VARIANT`` (int or ``auto``), ``IGG_DEBUG_SYNC``
+Framework knobs (new): ``IGG_TRANSPORT`` (``rccl`` | ``torch`` | ``staged``)
+for GPU point-to-point (``staged`` = host-staged gloo, the reference's
+non-GPU-aware path), ``IGG_STENCIL_VARIANT`` (int or ``auto``), ``IGG_DEBUG_SYNC``
 (synchronise after every halo update), ``IGG_QUIET``.
 """
 from __future__ import annotations
@@ -59,8 +60,8 @@ def parse_loopvectorization(env: Mapping[str, str] | None = None) -> list[bool]:
 def transport_choice(env: Mapping[str, str] | None = None) -> str:
     env = os.environ if env is None else env
     t = env.get("IGG_TRANSPORT", "rccl").strip().lower()
-    if t not in ("rccl", "torch"):
-        raise ValueError(f"IGG_TRANSPORT must be 'rccl' or 'torch' (got {t!r})")
+    if t not in ("rccl", "torch", "staged"):
+        raise ValueError(f"IGG_TRANSPORT must be 'rccl', 'torch' or 'staged' (got {t!r})")
     return t
 
 

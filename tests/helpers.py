@@ -27,3 +27,30 @@ def zero_boundaries(A: torch.Tensor) -> torch.Tensor:
         idx[d] = [0, A.shape[d] - 1]
         A[tuple(idx)] = 0
     return A
+
+
+def expected_after_halo(ref: torch.Tensor, fields_dim_has_halo, neighbors) -> torch.Tensor:
+    """Exact oracle of update_halo after zeroing every boundary plane.
+
+    An entry keeps its reference value iff, for every dim in which it lies on a
+    boundary plane (index 0 or n-1), the field has a halo in that dim and a
+    neighbour exists on that side; otherwise it stays 0 (x->y->z sequential
+    exchange carries corners only through existing neighbours).
+    ``fields_dim_has_halo[d]``: ol(d,A) >= 2; ``neighbors[s][d]``: rank or -1.
+    """
+    keep = torch.ones(ref.shape, dtype=torch.bool)
+    for d in range(ref.dim()):
+        n = ref.shape[d]
+        for side, idx in ((0, 0), (1, n - 1)):
+            ok = fields_dim_has_halo[d] and neighbors[side][d] != -1
+            if not ok:
+                sl = [slice(None)] * ref.dim()
+                sl[d] = idx
+                keep[tuple(sl)] = False
+    out = torch.zeros_like(ref)
+    out[keep] = ref[keep]
+    return out
+
+
+def has_halo(A, gg) -> list:
+    return [int(gg.overlaps[d]) + (A.shape[d] if A.dim() > d else 1) - int(gg.nxyz[d]) >= 2 for d in range(3)]

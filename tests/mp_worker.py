@@ -1,0 +1,157 @@
+"""Per-rank test scenarios (launched by tests/_mp.py, one process per rank)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import igg  # noqa: E402
+from tests.helpers import encode, expected_after_halo, has_halo, zero_boundaries  # noqa: E402
+
+DTYPES = {"f64": torch.float64, "f32": torch.float32, "f16": torch.float16, "c128": torch.complex128, "i16": torch.int16}
+
+
+def _device(kind):
+    if kind == "gpu":
+        torch.cuda.set_device(0)
+        return torch.device("cuda", 0)
+    return torch.device("cpu")
+
+
+def scenario_halo(dev, nx, ny, nz, px, py, pz, dt, dimx=0, dimy=0, dimz=0):
+    device = _device(dev)
+    nx, ny, nz, px, py, pz = map(int, (nx, ny, nz, px, py, pz))
+    dtype = DTYPES[dt]
+    igg.init_global_grid(nx, ny, nz, periodx=px, periody=py, periodz=pz, dimx=int(dimx), dimy=int(dimy),
+                         dimz=int(dimz), quiet=True, select_device=False,
+                         device_type="AMDGPU" if dev == "gpu" else "auto")
+    gg = igg.get_global_grid()
+    nd = 3 if nz > 1 else (2 if ny > 1 else 1)
+    base = (nx, ny, nz)[:nd]
+    deltas = [(0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1), (-1, 2, 1), (2, -1, 1)]
+    seen = set()
+    for dl in deltas:
+        shape = tuple(b + d for b, d in zip(base, dl[:nd]))
+        if shape in seen or min(shape) < 1:
+            continue
+        seen.add(shape)
+        A = torch.zeros(shape, dtype=dtype)
+        if not any(has_halo(A, gg)[:nd]):
+            continue
+        encode(A, complex_factor=(1 + 1j) if dtype.is_complex else None)
+        ref = expected_after_halo(A, has_halo(A, gg), gg.neighbors.tolist())
+        X = zero_boundaries(A.clone()).to(device)
+        igg.update_halo_(X)
+        got = X.cpu()
+        if not torch.equal(got, ref):
+            bad = (got != ref).nonzero()[:5].tolist()
+            raise AssertionError(f"rank {gg.me} shape {shape} dims {gg.dims.tolist()} mismatch at {bad}")
+    # two fields in one call (staggered Vx, Vz) + three fields of different sizes
+    if nd == 3:
+        fs = [torch.zeros(nx + 1, ny, nz, dtype=dtype), torch.zeros(nx, ny, nz + 1, dtype=dtype),
+              torch.zeros(nx, ny + 1, nz, dtype=dtype)]
+        refs = []
+        for F in fs:
+            encode(F, complex_factor=(1 + 1j) if dtype.is_complex else None)
+            refs.append(expected_after_halo(F, has_halo(F, gg), gg.neighbors.tolist()))
+        Xs = [zero_boundaries(F.clone()).to(device) for F in fs]
+        igg.update_halo_(*Xs)
+        for X, R in zip(Xs, refs):
+            assert torch.equal(X.cpu(), R), f"rank {gg.me}: multi-field mismatch"
+    igg.finalize_global_grid()
+    print(f"rank {gg.me} OK dims={gg.dims.tolist()}")
+
+
+def scenario_gather(dev, dt):
+    device = _device(dev)
+    dtype = DTYPES[dt]
+    nx, ny, nz = 4, 3, 2
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, quiet=True, select_device=False,
+                                                          device_type="AMDGPU" if dev == "gpu" else "auto")
+    for root in sorted({0, nprocs - 1}):
+        for shape in [(nx,), (nx, ny), (nx, ny, nz)]:
+            A = torch.full(shape, float(me + 1), dtype=dtype).to(device)
+            flat = torch.arange(A.numel(), dtype=torch.float64).view(shape).to(dtype).to(device)
+            A = A * 100 + flat
+            s = list(shape) + [1] * (3 - len(shape))
+            G = torch.zeros(dims[0] * s[0], dims[1] * s[1], dims[2] * s[2], dtype=dtype).to(device) if me == root else None
+            igg.gather_(A, G, root=root)
+            if me == root:
+                G = G.cpu()
+                for p in range(nprocs):
+                    c = igg.native.cart_coords(p, dims.tolist())
+                    blk = G[c[0] * s[0]:(c[0] + 1) * s[0], c[1] * s[1]:(c[1] + 1) * s[1], c[2] * s[2]:(c[2] + 1) * s[2]]
+                    exp = (torch.full(s, float(p + 1), dtype=torch.float64) * 100 +
+                           torch.arange(blk.numel(), dtype=torch.float64).view(s)).to(dtype)
+                    assert torch.equal(blk, exp), f"root {root}: block of rank {p} wrong"
+        # 1-D A gathered into a 3-D A_global (only the length must match)
+        A = torch.full((nx,), float(me), dtype=dtype).to(device)
+        G = torch.zeros(nx * dims[0], dims[1], dims[2], dtype=dtype).to(device) if me == root else None
+        igg.gather_(A, G, root=root)
+    igg.finalize_global_grid()
+    print(f"rank {me} gather OK")
+
+
+def scenario_diffusion(dev, nx, ny, nz, steps, overlap):
+    from igg.models.diffusion3d import Diffusion3D
+    from igg.ops import stencil
+
+    device = _device(dev)
+    nx, ny, nz, steps = int(nx), int(ny), int(nz), int(steps)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, quiet=True, select_device=False,
+                                                          device_type="AMDGPU" if dev == "gpu" else "auto")
+    gg = igg.get_global_grid()
+    m = Diffusion3D(dtype=torch.float64, device=device, overlap=bool(int(overlap)))
+    m.run(steps)
+    loc = m.T.cpu()
+    # global reference: same physics on the implicit global grid, one array
+    ng = [int(v) for v in gg.nxyz_g]
+    lx = ly = lz = 10.0
+    dx, dy, dz = lx / (ng[0] - 1), ly / (ng[1] - 1), lz / (ng[2] - 1)
+    x = (torch.arange(ng[0], dtype=torch.float64) * dx).view(-1, 1, 1)
+    y = (torch.arange(ng[1], dtype=torch.float64) * dy).view(1, -1, 1)
+    z = (torch.arange(ng[2], dtype=torch.float64) * dz).view(1, 1, -1)
+    Cp = 1 + 5 * torch.exp(-(x - lx / 1.5) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2) + \
+        5 * torch.exp(-(x - lx / 3.0) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2)
+    T = 100 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 3.0) / 2) ** 2) + \
+        50 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 1.5) / 2) ** 2)
+    for _ in range(steps):
+        T = stencil.diffusion3d_reference(T, Cp, lam=m.lam, dt=m.dt, dx=m.dx, dy=m.dy, dz=m.dz)
+    o = [int(coords[d]) * (int(gg.nxyz[d]) - int(gg.overlaps[d])) for d in range(3)]
+    blk = T[o[0]:o[0] + nx, o[1]:o[1] + ny, o[2]:o[2] + nz]
+    err = (loc - blk).abs().max().item()
+    assert err < 1e-10, f"rank {me}: diffusion mismatch {err}"
+    igg.finalize_global_grid()
+    print(f"rank {me} diffusion OK err={err:.2e}")
+
+
+def scenario_ring(dev):
+    """Transport-level ring exchange (test_update_halo.jl:697-743 analogue)."""
+    device = _device(dev)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 4, 4, dimx=0, dimy=1, dimz=1, periodx=1, quiet=True,
+                                                          select_device=False,
+                                                          device_type="AMDGPU" if dev == "gpu" else "auto")
+    gg = igg.get_global_grid()
+    left, right = int(gg.neighbors[0, 0]), int(gg.neighbors[1, 0])
+    send = torch.full((16,), float(me), dtype=torch.float64, device=device)
+    recv = torch.zeros(32, dtype=torch.float64, device=device)
+    t = comm.host_transport() if dev == "cpu" else comm.device_transport()
+    recvs = [(recv.data_ptr() + 128, 128, right, 1), (recv.data_ptr(), 128, left, 0)]
+    sends = [(send.data_ptr(), 128, left, 1), (send.data_ptr(), 128, right, 0)]
+    fn = {"gloo": comm._gloo_p2p, "gloo-staged": comm._staged_p2p}.get(t.name)
+    if fn is None:
+        raise SystemExit(0)
+    fn(recvs, sends, dev == "gpu", torch.cuda.current_stream().cuda_stream if dev == "gpu" else 0)
+    if dev == "gpu":
+        torch.cuda.synchronize()
+    r = recv.cpu()
+    assert (r[:16] == left).all() and (r[16:] == right).all(), f"rank {me}: ring wrong {r}"
+    igg.finalize_global_grid()
+    print(f"rank {me} ring OK")
+
+
+if __name__ == "__main__":
+    name, *args = sys.argv[1:]
+    globals()[f"scenario_{name}"](*args)

@@ -1,0 +1,68 @@
+"""Multi-rank tests on CPU (gloo, world sizes 2..8) — the reference suite's
+"any number of processes" mode, with an exact per-entry oracle."""
+import pytest
+
+from tests._mp import run_ranks
+
+
+@pytest.mark.parametrize("nprocs,cfg", [
+    (2, (7, 5, 6, 0, 0, 0)),
+    (2, (7, 5, 6, 1, 1, 1)),   # dims 2x1x1 periodic: left == right neighbour
+    (4, (7, 5, 6, 1, 0, 1)),
+    (8, (7, 5, 6, 0, 0, 0)),   # 2x2x2
+    (3, (7, 5, 6, 1, 1, 1)),
+])
+def test_halo_cpu_multirank(nprocs, cfg):
+    run_ranks(nprocs, "halo", "cpu", *cfg, "f64")
+
+
+@pytest.mark.parametrize("nprocs,cfg,dims", [
+    (2, (7, 1, 1, 1, 0, 0), (0, 1, 1)),   # 1-D
+    (4, (7, 5, 1, 1, 1, 0), (0, 0, 1)),   # 2-D 2x2 periodic
+    (4, (7, 5, 6, 0, 1, 0), (1, 4, 1)),   # 4 ranks along y
+])
+def test_halo_cpu_lowdim(nprocs, cfg, dims):
+    run_ranks(nprocs, "halo", "cpu", *cfg, "f32", *dims)
+
+
+def test_halo_cpu_complex():
+    run_ranks(2, "halo", "cpu", 7, 5, 6, 1, 1, 1, "c128")
+
+
+@pytest.mark.parametrize("nprocs", [2, 4])
+def test_gather_cpu_multirank(nprocs):
+    run_ranks(nprocs, "gather", "cpu", "f64")
+
+
+def test_gather_cpu_int16():
+    run_ranks(2, "gather", "cpu", "i16")
+
+
+@pytest.mark.parametrize("nprocs,overlap", [(2, 0), (8, 0)])
+def test_diffusion_cpu_multirank_matches_global(nprocs, overlap):
+    run_ranks(nprocs, "diffusion", "cpu", 10, 9, 8, 4, overlap)
+
+
+def test_ring_cpu():
+    run_ranks(3, "ring", "cpu")
+
+
+# --- same scenarios with GPU fields, several ranks sharing the one GPU via the
+# host-staged transport (exercises the HIP pack/unpack kernels across ranks).
+GPU_ENV = {"IGG_TRANSPORT": "staged"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,cfg", [(2, (7, 5, 6, 1, 1, 1)), (8, (7, 5, 6, 0, 0, 0)), (4, (9, 6, 5, 1, 0, 1))])
+def test_halo_gpu_multirank_staged(nprocs, cfg):
+    run_ranks(nprocs, "halo", "gpu", *cfg, "f64", env_extra=GPU_ENV)
+
+
+@pytest.mark.gpu
+def test_diffusion_gpu_multirank_staged_overlap():
+    run_ranks(8, "diffusion", "gpu", 24, 20, 18, 5, 1, env_extra=GPU_ENV)
+
+
+@pytest.mark.gpu
+def test_gather_gpu_multirank_staged():
+    run_ranks(4, "gather", "gpu", "f64", env_extra=GPU_ENV)
