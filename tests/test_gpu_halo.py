@@ -128,3 +128,49 @@ def test_gpu_gather_reorder_kernel(gpu):
     torch.cuda.synchronize()
     ref = src.view(*dims, *s).permute(0, 3, 1, 4, 2, 5).reshape(-1)
     assert torch.equal(dst, ref)
+
+
+def _native_fields(*ts):
+    from igg.parallel.halo import field_tuple
+
+    return [field_tuple(t) for t in ts]
+
+
+def test_gpu_rccl_remote_path_via_self_peer(gpu):
+    """Full remote exchange path on RCCL in one process: the engine believes it
+    is rank 1 while both neighbours in every dim are rank 0, so every face goes
+    pack -> grouped ncclSend/ncclRecv (peer 0 = this process) -> unpack, with
+    left == right == same peer (the dims==2 periodic ordering case)."""
+    from igg._native import native
+
+    n = (9, 7, 8)
+    igg.init_global_grid(*n, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    A = encode(torch.zeros(n[0], n[1], n[2] + 1, dtype=torch.float64))
+    B = encode(torch.zeros(n[0] + 1, n[1], n[2], dtype=torch.float64))
+    refs = [A.clone(), B.clone()]
+    Ag, Bg = zero_boundaries(A.clone()).to(gpu), zero_boundaries(B.clone()).to(gpu)
+    gi = native.GridInfo(1, 2, list(n), [2, 2, 2], [[0, 0, 0], [0, 0, 0]])
+    eng = native.HaloEngine(gi)
+    comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
+    eng.set_transport(comm, True)
+    eng.exchange(_native_fields(Ag, Bg), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    comm.check_async_error()
+    assert torch.equal(Ag.cpu(), refs[0])
+    assert torch.equal(Bg.cpu(), refs[1])
+    del eng, comm
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_gpu_rccl_p2p_and_barrier(gpu):
+    from igg._native import native
+
+    comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
+    src = torch.arange(1000, dtype=torch.float32, device=gpu)
+    dst = torch.zeros_like(src)
+    s = torch.cuda.current_stream().cuda_stream
+    comm.p2p([(dst.data_ptr(), 4000, 0)], [(src.data_ptr(), 4000, 0)], s)
+    comm.barrier(s)
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    assert native.rccl_version().count(".") == 2
