@@ -283,3 +283,59 @@ def halo_plan_summary(*fields) -> list[dict]:
                 entry["faces"].append({"field": i + 1, "side": s + 1, "bytes": info[6], "zero_copy": bool(info[5])})
         out.append(entry)
     return out
+
+
+def _buf_view(which: int, n: int, dim: int, i: int, A: torch.Tensor, flat: bool):
+    bufs = _bufs(which, A.is_cuda)
+    if bufs is None:
+        raise IGGError("The halo buffers are not allocated.")
+    shape = halosize(dim, A)
+    numel = int(np.prod(shape))
+    b = bufs[i - 1][n - 1]
+    v = b.view(torch.uint8)[: b.numel() * b.element_size()].view(A.dtype)[:numel]
+    return v if flat else v.view(shape)
+
+
+def sendbuf_flat(n: int, dim: int, i: int, A: torch.Tensor):
+    """Flat send buffer of field slot ``i`` (1-based), side ``n``, typed as ``A``."""
+    return _buf_view(0, n, dim, i, A, True)
+
+
+def recvbuf_flat(n: int, dim: int, i: int, A: torch.Tensor):
+    return _buf_view(1, n, dim, i, A, True)
+
+
+def sendbuf(n: int, dim: int, i: int, A: torch.Tensor):
+    """Send buffer shaped like the halo of ``A`` in ``dim`` (update_halo.jl:288-290)."""
+    return _buf_view(0, n, dim, i, A, False)
+
+
+def recvbuf(n: int, dim: int, i: int, A: torch.Tensor):
+    return _buf_view(1, n, dim, i, A, False)
+
+
+def _face_copy(buf: torch.Tensor, A: torch.Tensor, ranges, dim: int, pack: bool) -> None:
+    if buf.dtype != A.dtype or buf.device != A.device:
+        raise IGGError("buffer and array must have the same element type and device")
+    idx = ranges[dim - 1].start - 1
+    ft = field_tuple(A)
+    base, n_outer, n_inner, s_outer, s_inner, _contig, nbytes = native.face_info(ft, dim - 1, idx)
+    if buf.numel() * buf.element_size() < nbytes or not buf.is_contiguous():
+        raise IGGError("buffer too small or not contiguous")
+    if pack:
+        c = (base, buf.data_ptr(), n_outer, n_inner, s_outer, s_inner, n_inner, 1)
+    else:
+        c = (buf.data_ptr(), base, n_outer, n_inner, n_inner, 1, s_outer, s_inner)
+    stream = torch.cuda.current_stream().cuda_stream if A.is_cuda else 0
+    native.copy2d([c], A.element_size(), A.is_cuda, stream)
+
+
+def write_face(buf: torch.Tensor, A: torch.Tensor, ranges, dim: int) -> None:
+    """Pack the plane ``ranges`` (1-based, single index in ``dim``) of ``A`` into
+    ``buf`` (reference write_h2h!/write_d2x!, update_halo.jl:569-612)."""
+    _face_copy(buf, A, ranges, dim, True)
+
+
+def read_face(buf: torch.Tensor, A: torch.Tensor, ranges, dim: int) -> None:
+    """Unpack ``buf`` into the plane ``ranges`` of ``A`` (read_h2h!/read_x2d!)."""
+    _face_copy(buf, A, ranges, dim, False)
