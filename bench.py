@@ -13,7 +13,7 @@ topology comes from init_global_grid (2 GPUs -> 2x1x1, 4 -> 2x2x1,
 8 -> 2x2x2); every step = fused stencil + update_halo_ (overlapped).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n 512]
-                       [--dtype float64] [--no-overlap] [--variant V|auto]
+                       [--dtype float64] [--overlap] [--variant V|auto]
 """
 from __future__ import annotations
 
@@ -35,9 +35,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=512, help="local grid points per dimension")
     ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
-    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--overlap", action="store_true", help="boundary/interior split with the halo on a second stream")
     ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
     ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
+    ap.add_argument("--loopback", action="store_true",
+                    help="1 GPU: route all 6 faces through the RCCL remote path to itself (interior-rank emulation)")
     return ap.parse_args()
 
 
@@ -58,7 +60,11 @@ def main():
     per = 1 if args.periodic else 0
     me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, n, periodx=per, periody=per, periodz=per,
                                                          quiet=True)
-    model = Diffusion3D(dtype=dtype, overlap=not args.no_overlap)
+    if args.loopback:
+        from igg.parallel.halo import enable_loopback
+
+        enable_loopback()
+    model = Diffusion3D(dtype=dtype, overlap=args.overlap)
     for _ in range(args.warmup):
         model.step()
     torch.cuda.synchronize()
@@ -109,6 +115,7 @@ def main():
                 "transport": os.environ.get("IGG_TRANSPORT", "rccl") if nprocs > 1 else "none",
                 "stencil_variant": os.environ.get("IGG_STENCIL_VARIANT", "0"),
                 "finite": finite,
+                "loopback_emulation": bool(args.loopback),
             },
         }
         print(json.dumps(out), flush=True)

@@ -151,6 +151,22 @@ PYBIND11_MODULE(_igg_native, m) {
     return py::bytes(out);
   });
   m.def("rccl_version", &rccl_version);
+  // Stream-ordered blocking copies for the host-staged transport: wait for all
+  // prior work on `stream`, copy, wait again.
+  m.def("memcpy_d2h_stream", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
+    py::gil_scoped_release nogil;
+    IGG_HIP_CHECK(hipStreamSynchronize(as_stream(s)));
+    IGG_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n,
+                                 hipMemcpyDeviceToHost, as_stream(s)));
+    IGG_HIP_CHECK(hipStreamSynchronize(as_stream(s)));
+  });
+  m.def("memcpy_h2d_stream", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
+    py::gil_scoped_release nogil;
+    IGG_HIP_CHECK(hipStreamSynchronize(as_stream(s)));
+    IGG_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n,
+                                 hipMemcpyHostToDevice, as_stream(s)));
+    IGG_HIP_CHECK(hipStreamSynchronize(as_stream(s)));
+  });
 
   // --- field geometry helpers (test hooks)
   m.def("ol", [](const GridInfo& g, int dim, const FieldTuple& f) { return ol(g, dim, to_field(f)); });
@@ -299,8 +315,8 @@ PYBIND11_MODULE(_igg_native, m) {
   m.def("diffusion3d",
         [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
            double dtlam, int elem_bytes, const std::vector<std::pair<Int3, Int3>>& boxes,
-           bool device, int variant, uintptr_t stream) {
-          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes};
+           bool device, int variant, uintptr_t stream, int rounds) {
+          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes, rounds};
           const auto bx = to_boxes(boxes);
           if (device) {
             launch_diffusion3d(a, bx, variant, as_stream(stream));
@@ -311,7 +327,7 @@ PYBIND11_MODULE(_igg_native, m) {
         },
         py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
         py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
-        py::arg("stream") = 0);
+        py::arg("stream") = 0, py::arg("rounds") = 0);
   m.def("split_boundary", [](const Int3& n, const std::array<bool, 3>& active, const Int3& w) {
     std::vector<Box> slabs;
     Box interior;

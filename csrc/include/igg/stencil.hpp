@@ -30,6 +30,8 @@ struct DiffusionArgs {
   double rd2[3];            // 1/dx_d^2
   double dt_lam;            // dt*lam
   int elem_bytes;           // 8 (f64) or 4 (f32)
+  int rounds = 0;           // grid sizing for this launch: 0 = global default,
+                            // k > 0 = k residency rounds, k < 0 = |k|*4096 blocks
 };
 
 // Number of tuned kernel variants (see stencil_kernels.hip); variant 0 = default.

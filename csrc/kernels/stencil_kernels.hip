@@ -172,10 +172,19 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
   const int64_t lo2 = bt.lo[k][2], hi2 = bt.hi[k][2];
   const int64_t n2 = a.n2, s1 = a.n2, s0 = a.n1 * a.n2;
   const int64_t z0 = zt + lane * VZ;
-  const int zl = static_cast<int>(min(z0, n2 - VZ) - zt);    // per-lane offset in the tile
-  const bool lane_full = z0 >= lo2 && z0 + VZ <= hi2;
   if (zt >= hi2) return;  // whole wave segment past the box (partial last tile)
-  const int64_t zem = max<int64_t>(zt - 1, 0) - zt, zep = min<int64_t>(zt + 64 * VZ, n2 - 1) - zt;
+  // Lanes whose vector holds no box point alias the first/last vector that does,
+  // so a thin box (a single send plane) touches only the lines it needs.
+  const int64_t zlo_v = (lo2 / VZ) * VZ, zhi_v = ((hi2 - 1) / VZ) * VZ;
+  const int64_t zc = min(max(z0, zlo_v), zhi_v);
+  const int zl = static_cast<int>(zc - zt);                  // per-lane offset in the tile
+  const bool lane_full = z0 >= lo2 && z0 + VZ <= hi2;
+  // z-neighbours come from lane neighbours except where that neighbour lane is
+  // clamped (or outside the wave): those lanes load their edge value directly.
+  const bool load_prev = lane == 0 || z0 - VZ < zlo_v;
+  const bool load_next = lane == 63 || z0 + VZ > zhi_v;
+  const int zpi = static_cast<int>(max<int64_t>(zc - 1, 0) - zt);
+  const int zni = static_cast<int>(min<int64_t>(zc + VZ, n2 - 1) - zt);
 
   int64_t rowb[RY];  // wave-uniform row bases (element index of the tile origin)
 #pragma unroll
@@ -209,8 +218,8 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
     T em[RY], ep[RY];
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
-      em[r] = t[off + rowb[r] + zem];
-      ep[r] = t[off + rowb[r] + zep];
+      em[r] = load_prev ? t[off + rowb[r] + zpi] : T(0);
+      ep[r] = load_next ? t[off + rowb[r] + zni] : T(0);
     }
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
@@ -219,8 +228,8 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
       const V& yn = (r + 1 < nv) ? tc[(r + 1 < RY) ? r + 1 : r] : yp;
       T prev = __shfl_up(c[VZ - 1], 1);
       T next = __shfl_down(c[0], 1);
-      if (lane == 0) prev = em[r];
-      if (lane == 63) next = ep[r];
+      if (load_prev) prev = em[r];
+      if (load_next) next = ep[r];
       V out;
 #pragma unroll
       for (int e = 0; e < VZ; ++e) {
@@ -239,7 +248,7 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
         } else {
 #pragma unroll
           for (int e = 0; e < VZ; ++e)
-            if (z0 + e >= lo2 && z0 + e < hi2 && zt + zl == z0) dst[e] = out[e];
+            if (z0 + e >= lo2 && z0 + e < hi2 && zc == z0) dst[e] = out[e];
         }
       }
     }
@@ -289,6 +298,9 @@ constexpr Variant VARIANTS[] = {
     {"v2_bz2_by4_ry8_nt", 4, 8, 2, false, true}, // 15
     {"v4_bz2_by8_ry2_nt", 8, 2, 4, false, true}, // 16
     {"v2_bz4_by4_ry4_nt", 4, 4, 2, false, true}, // 17
+    {"s_by4_ry1", 4, 1, 1, false, false},        // 18 (low-VGPR: thin send planes)
+    {"v2_by4_ry1_nt", 4, 1, 2, false, true},     // 19 (low-VGPR vector)
+    {"v4_by4_ry2", 4, 2, 4, false, false},       // 20
 };
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
@@ -296,6 +308,7 @@ constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 // occupancy x CUs); the x-march is chunked so every block gets equal work and
 // no partial last round leaves CUs idle. g_rounds <= 0: fixed 4096-block target.
 int g_rounds = 1;
+int g_call_rounds = 0;  // per-launch override (set by launch_diffusion3d for one call)
 
 int resident_blocks(const void* kernel, int block) {
   static std::vector<std::pair<const void*, int>> cache;
@@ -355,8 +368,9 @@ void for_each_table(const std::vector<Box>& boxes, int W, int TY, bool aligned, 
 }
 
 int64_t target_for(const void* kernel, int block) {
-  if (g_rounds <= 0) return 4096;
-  return static_cast<int64_t>(g_rounds) * resident_blocks(kernel, block);
+  const int rounds = g_call_rounds != 0 ? g_call_rounds : g_rounds;
+  if (rounds <= 0) return 4096 * (rounds < 0 ? -rounds : 1);
+  return static_cast<int64_t>(rounds) * resident_blocks(kernel, block);
 }
 
 template <typename T, int BY, int RY, bool XCD>
@@ -403,6 +417,9 @@ void dispatch(const KArgs<T>& ka, const std::vector<Box>& boxes, int v, hipStrea
     case 15: launch_vector<T, 4, 8, 2, false, true, 2>(ka, boxes, s); break;
     case 16: launch_vector<T, 8, 2, 4, false, true, 2>(ka, boxes, s); break;
     case 17: launch_vector<T, 4, 4, 2, false, true, 4>(ka, boxes, s); break;
+    case 18: launch_scalar<T, 4, 1, true>(ka, boxes, s); break;
+    case 19: launch_vector<T, 4, 1, 2, false, true>(ka, boxes, s); break;
+    case 20: launch_vector<T, 4, 2, 4, false, false>(ka, boxes, s); break;
     default: fail("diffusion3d: invalid kernel variant ", v);
   }
 }
@@ -432,6 +449,10 @@ const char* diffusion3d_variant_name(int v) {
 
 void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, int variant,
                         hipStream_t stream) {
+  struct RoundsGuard {
+    explicit RoundsGuard(int r) { g_call_rounds = r; }
+    ~RoundsGuard() { g_call_rounds = 0; }
+  } guard(a.rounds);
   if (a.n[0] < 3 || a.n[1] < 3 || a.n[2] < 3) fail("diffusion3d: every extent must be >= 3");
   for (const Box& b : boxes)
     for (int d = 0; d < 3; ++d)

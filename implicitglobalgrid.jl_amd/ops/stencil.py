@@ -76,8 +76,12 @@ def autotune(T2, T, Cp, rd2, dtlam, boxes, reps: int = 5) -> int:
 
 
 def diffusion3d_(T2, T, Cp, *, lam: float, dt: float, dx: float, dy: float, dz: float,
-                 boxes=None, variant: int | None = None, stream: int | None = None) -> None:
-    """One fused diffusion update of ``T2`` from ``T`` on ``boxes`` (default: whole interior)."""
+                 boxes=None, variant: int | None = None, stream: int | None = None, rounds: int = 0) -> None:
+    """One fused diffusion update of ``T2`` from ``T`` on ``boxes`` (default: whole interior).
+
+    ``rounds`` sizes the grid of this launch: 0 = library default, k > 0 = k
+    residency rounds (k x resident workgroups), k < 0 = |k| x 4096 workgroups.
+    """
     _check(T2, T, Cp)
     rd2 = [1.0 / (dx * dx), 1.0 / (dy * dy), 1.0 / (dz * dz)]
     dtlam = dt * lam
@@ -91,7 +95,7 @@ def diffusion3d_(T2, T, Cp, *, lam: float, dt: float, dx: float, dy: float, dz: 
     else:
         s, v = 0, 0
     native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), list(T.shape), rd2, dtlam,
-                       T.element_size(), boxes, dev, v, s)
+                       T.element_size(), boxes, dev, v, s, rounds)
 
 
 def diffusion3d_reference(T, Cp, *, lam, dt, dx, dy, dz) -> torch.Tensor:

@@ -183,17 +183,18 @@ class Communicator:
     def _staged_p2p(self, recvs, sends, device, stream):
         """Host-staged device exchange (the reference's non-GPU-aware MPI path,
         update_halo.jl:437,465): D2H of the send buffers, gloo, H2D."""
-        s = torch.cuda.ExternalStream(stream)
-        with torch.cuda.stream(s):
-            hs = [(_device_view(p, n).cpu(), peer, tag) for p, n, peer, tag in sends]
-            hr = [(torch.empty(n, dtype=torch.uint8), p, peer, tag) for p, n, peer, tag in recvs]
+        hs = []
+        for p, n, peer, tag in sends:
+            h = torch.empty(n, dtype=torch.uint8)
+            native.memcpy_d2h_stream(h.data_ptr(), p, n, stream)
+            hs.append((h, peer, tag))
+        hr = [(torch.empty(n, dtype=torch.uint8), p, peer, tag) for p, n, peer, tag in recvs]
         reqs = [dist.irecv(h, src=self.global_rank(peer), group=self.gloo, tag=tag) for h, _p, peer, tag in hr]
         reqs += [dist.isend(h, dst=self.global_rank(peer), group=self.gloo, tag=tag) for h, peer, tag in hs]
         for r in reqs:
             r.wait()
-        with torch.cuda.stream(s):
-            for h, p, _peer, _tag in hr:
-                _device_view(p, h.numel()).copy_(h, non_blocking=False)
+        for h, p, _peer, _tag in hr:
+            native.memcpy_h2d_stream(p, h.data_ptr(), h.numel(), stream)
 
     def _torch_p2p(self, recvs, sends, device, stream):
         ops = []

@@ -78,11 +78,12 @@ def _init_engine(gg) -> None:
 
 
 def _drop_engine() -> None:
-    global _engine
+    global _engine, _loopback_comm
     _plans.clear()
     if _engine is not None:
         _engine.pool_free()
     _engine = None
+    _loopback_comm = None
 
 
 def engine():
@@ -94,6 +95,34 @@ def sync_grid() -> None:
     """Push the (possibly test-mutated) grid topology into the native engine."""
     _plans.clear()
     _engine.set_grid(_grid_info(_grid.global_grid()))
+
+
+_loopback_comm = None
+
+
+def enable_loopback(dims=(True, True, True)) -> None:
+    """Single-GPU emulation of a rank surrounded by neighbours (perf analysis).
+
+    Every selected dimension gets both neighbours = rank 0 while the engine
+    believes it is rank 1, so each face takes the full remote path — pack ->
+    grouped ncclSend/ncclRecv over a 1-rank RCCL communicator (to itself) ->
+    unpack — with real RCCL kernels competing for CUs, exactly like an
+    interior rank of a multi-GPU run. The grid's neighbour table is updated
+    too, so apps enable their boundary/interior overlap. Results equal a
+    periodic exchange.
+    """
+    global _loopback_comm
+    gg = _grid.global_grid()
+    if gg.nprocs != 1 or not gg.amdgpu_enabled:
+        raise IGGError("loopback mode needs a single-process grid with a GPU")
+    for d in range(NDIMS):
+        if dims[d]:
+            gg.neighbors[:, d] = 0
+    _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
+    nb = gg.neighbors.tolist()
+    _engine.set_grid(native.GridInfo(1, 2, gg.nxyz.tolist(), gg.overlaps.tolist(), nb))
+    _engine.set_transport(_loopback_comm, True)
+    _plans.clear()
 
 
 # --- argument checks (update_halo.jl:804-834) ---------------------------------
