@@ -49,13 +49,18 @@ std::vector<Field> to_fields(const std::vector<FieldTuple>& ts) {
 }
 
 GridInfo make_grid(int64_t me, int64_t nprocs, const Int3& nxyz, const Int3& overlaps,
-                   const std::array<Int3, 2>& neighbors) {
+                   const std::array<Int3, 2>& neighbors, const std::vector<int64_t>& peers) {
   GridInfo g;
   g.me = me;
   g.nprocs = nprocs;
   g.nxyz = nxyz;
   g.overlaps = overlaps;
   g.neighbors = neighbors;
+  if (!peers.empty()) {
+    if (peers.size() != 27) fail("GridInfo: peers must have 27 entries (dir_key order)");
+    for (int k = 0; k < 27; ++k) g.peers[k] = peers[k];
+    g.has_peers = true;
+  }
   return g;
 }
 
@@ -185,7 +190,9 @@ PYBIND11_MODULE(_igg_native, m) {
 
   py::class_<GridInfo>(m, "GridInfo")
       .def(py::init(&make_grid), py::arg("me"), py::arg("nprocs"), py::arg("nxyz"),
-           py::arg("overlaps"), py::arg("neighbors"))
+           py::arg("overlaps"), py::arg("neighbors"), py::arg("peers") = std::vector<int64_t>{})
+      .def_readonly("peers", &GridInfo::peers)
+      .def_readonly("has_peers", &GridInfo::has_peers)
       .def_readwrite("me", &GridInfo::me)
       .def_readwrite("nprocs", &GridInfo::nprocs)
       .def_readwrite("nxyz", &GridInfo::nxyz)
@@ -260,6 +267,12 @@ PYBIND11_MODULE(_igg_native, m) {
            [](HaloEngine& e, const std::vector<FieldTuple>& fs, uintptr_t s) {
              e.exchange(to_fields(fs), as_stream(s));
            })
+      .def("set_mode", [](HaloEngine& e, int m) { e.set_mode(static_cast<HaloMode>(m)); })
+      .def_property_readonly("mode", [](HaloEngine& e) { return static_cast<int>(e.mode()); })
+      .def("resolved_mode", [](HaloEngine& e, const FieldSet& fs) {
+        return static_cast<int>(e.resolved_mode(fs.f));
+      })
+      .def_property_readonly("last_message_count", &HaloEngine::last_message_count)
       .def("exchange_set",
            [](HaloEngine& e, const FieldSet& fs, uintptr_t s) { e.exchange(fs.f, as_stream(s)); })
       .def("exchange_dim",

@@ -59,9 +59,44 @@ Face face(const Field& f, int dim, int64_t index) {
   return fc;
 }
 
+Face region_face(const Field& f, const Region& r) {
+  int ext[2] = {-1, -1}, k = 0;
+  for (int d = 0; d < NDIMS; ++d)
+    if (r.hi[d] - r.lo[d] > 1) {
+      if (k == 2) fail("region_face: region has three non-singleton extents");
+      ext[k++] = d;
+    }
+  Face fc{};
+  int64_t off = 0;
+  for (int d = 0; d < NDIMS; ++d) off += r.lo[d] * f.stride[d];
+  fc.base = reinterpret_cast<char*>(f.ptr) + off * f.elem_bytes;
+  int inner = -1, outer = -1;
+  if (k == 2) {
+    inner = f.stride[ext[0]] < f.stride[ext[1]] ? ext[0] : ext[1];
+    outer = inner == ext[0] ? ext[1] : ext[0];
+  } else if (k == 1) {
+    inner = ext[0];
+  }
+  fc.n_inner = inner >= 0 ? r.hi[inner] - r.lo[inner] : 1;
+  fc.s_inner = inner >= 0 ? f.stride[inner] : 1;
+  fc.n_outer = outer >= 0 ? r.hi[outer] - r.lo[outer] : 1;
+  fc.s_outer = outer >= 0 ? f.stride[outer] : fc.n_inner * fc.s_inner;
+  if (fc.n_inner == 1) fc.s_inner = 1;
+  if (fc.n_outer == 1) fc.s_outer = fc.n_inner * fc.s_inner;
+  fc.contiguous = fc.s_inner == 1 && fc.s_outer == fc.n_inner;
+  fc.bytes = static_cast<size_t>(fc.n_outer * fc.n_inner * f.elem_bytes);
+  return fc;
+}
+
 // ---------------------------------------------------------------- BufferPool
 
 BufferPool::~BufferPool() { free_all(); }
+
+char* BufferPool::arena(int which, size_t bytes, bool device) {
+  Buf& b = arena_[device ? 1 : 0][which];
+  if (b.bytes < bytes) grow(b, round_up(static_cast<int64_t>(bytes), 1 << 16), device);
+  return b.p;
+}
 
 void BufferPool::grow(Buf& b, size_t bytes, bool device) {
   if (b.bytes >= bytes) return;
@@ -121,6 +156,8 @@ void BufferPool::free_all() {
     for (int n = 0; n < NNEIGHBORS; ++n) { release(s.send[n], false); release(s.recv[n], false); }
   for (auto& s : dev_)
     for (int n = 0; n < NNEIGHBORS; ++n) { release(s.send[n], true); release(s.recv[n], true); }
+  for (int dv = 0; dv < 2; ++dv)
+    for (int w = 0; w < 2; ++w) release(arena_[dv][w], dv == 1);
   host_.clear();
   dev_.clear();
   host_alloc_ = dev_alloc_ = false;
@@ -144,7 +181,12 @@ void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) 
     // ran on another stream.
     if (have_event_ && last_stream_ != stream) IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_, 0));
   }
-  for (int dim = 0; dim < NDIMS; ++dim) exchange_dim_impl(fields, dim, device, stream);
+  if (resolved_mode(fields) == HaloMode::OnePhase) {
+    exchange_onephase(fields, device, stream);
+  } else {
+    last_msgs_ = 0;
+    for (int dim = 0; dim < NDIMS; ++dim) exchange_dim_impl(fields, dim, device, stream);
+  }
   if (device) {
     IGG_HIP_CHECK(hipEventRecord(done_, stream));
     have_event_ = true;
@@ -235,6 +277,157 @@ void HaloEngine::exchange_dim_impl(const std::vector<Field>& fields, int dim, bo
   }
   do_copies(pack);
   transport_->exchange(recvs, sends, device, stream);
+  do_copies(unpack);
+}
+
+}  // namespace igg
+
+// ------------------------------------------------------- one-phase exchange
+//
+// Equivalence with the sequential x -> y -> z schedule (reference
+// update_halo.jl:40): with sequential faces spanning the full extent of the
+// other dims, the value finally landing at a halo position p comes from the
+// rank at coords + v, where v_d = -1/+1 for every dim d in which p lies on the
+// left/right halo plane (with a neighbour there), read at that rank's send
+// plane in those dims and at p in the others. The one-phase schedule sends
+// exactly these values directly: one message per direction v (faces |v|=1,
+// edges |v|=2, corners |v|=3). In a dim d with v_d = 0 a message covers
+// [lo_d, hi_d) where the halo planes are excluded iff a neighbour exists on that
+// side (those positions belong to the message of a longer direction), so all
+// receive regions are disjoint and unpacking needs no ordering. Sender and
+// receiver agree on the extents because they share the coordinate in every dim
+// with v_d = 0, hence the same neighbour existence there.
+
+namespace igg {
+
+bool HaloEngine::active(const Field& f, int d) const {
+  return ol(grid_, d, f) >= 2 &&
+         (grid_.neighbors[0][d] != PROC_NULL || grid_.neighbors[1][d] != PROC_NULL);
+}
+
+HaloMode HaloEngine::resolved_mode(const std::vector<Field>& fields) const {
+  if (mode_ != HaloMode::Auto) return mode_;
+  if (!grid_.has_peers) return HaloMode::Sequential;
+  for (int d = 0; d < NDIMS; ++d)
+    for (int s = 0; s < NNEIGHBORS; ++s) {
+      const int64_t nb = grid_.neighbors[s][d];
+      if (nb != PROC_NULL && nb != grid_.me) return HaloMode::OnePhase;
+    }
+  (void)fields;
+  return HaloMode::Sequential;
+}
+
+namespace {
+struct Msg {
+  size_t field;
+  int key;  // direction as seen by the receiver
+  int64_t peer;
+  Face face;
+  size_t off;
+  bool zero_copy;
+};
+constexpr size_t MSG_ALIGN = 256;
+}  // namespace
+
+void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device,
+                                   hipStream_t stream) {
+  const GridInfo& g = grid_;
+  if (!g.has_peers) fail("one-phase halo exchange needs the peer table (GridInfo.peers)");
+  std::vector<Msg> sends, recvs;
+  size_t send_bytes = 0, recv_bytes = 0;
+  bool any_remote = false;
+  for (int key = 0; key < 27; ++key) {
+    if (key == 13) continue;
+    const int u[3] = {key / 9 - 1, (key / 3) % 3 - 1, key % 3 - 1};  // receiver-side direction
+    const int64_t from = g.peers[key];                 // I receive from coords + u
+    const int64_t to = g.peers[26 - key];              // I send in direction -u
+    for (size_t i = 0; i < fields.size(); ++i) {
+      const Field& f = fields[i];
+      bool ok = true;
+      Region rr{}, sr{};
+      for (int d = 0; d < NDIMS && ok; ++d) {
+        const int64_t n = f.size[d];
+        if (u[d] != 0) {
+          if (!active(f, d)) { ok = false; break; }
+          const int64_t o = ol(g, d, f);
+          // receive into my halo plane on side u_d; the matching send (direction
+          // -u) reads my send plane on side -u_d.
+          rr.lo[d] = u[d] < 0 ? 0 : n - 1;
+          sr.lo[d] = u[d] < 0 ? n - o : o - 1;
+        } else {
+          const bool act = active(f, d);
+          rr.lo[d] = (act && g.neighbors[0][d] != PROC_NULL) ? 1 : 0;
+          const int64_t hi = (act && g.neighbors[1][d] != PROC_NULL) ? n - 1 : n;
+          rr.hi[d] = hi;
+          sr.lo[d] = rr.lo[d];
+          sr.hi[d] = hi;
+          continue;
+        }
+        rr.hi[d] = rr.lo[d] + 1;
+        sr.hi[d] = sr.lo[d] + 1;
+      }
+      if (!ok || rr.count() <= 0) continue;
+      if (from != PROC_NULL) {
+        Msg m{i, key, from, region_face(f, rr), 0, false};
+        m.zero_copy = m.face.contiguous && from != g.me;
+        if (!m.zero_copy) { m.off = recv_bytes; recv_bytes += round_up(m.face.bytes, MSG_ALIGN); }
+        any_remote |= from != g.me;
+        recvs.push_back(m);
+      }
+      if (to != PROC_NULL) {
+        Msg m{i, key, to, region_face(f, sr), 0, false};
+        m.zero_copy = m.face.contiguous && to != g.me;
+        if (!m.zero_copy) { m.off = send_bytes; send_bytes += round_up(m.face.bytes, MSG_ALIGN); }
+        sends.push_back(m);
+      }
+    }
+  }
+  last_msgs_ = static_cast<int>(sends.size());
+  if (sends.empty() && recvs.empty()) return;
+  const std::shared_ptr<Transport>& tr = device ? dev_transport_ : host_transport_;
+  if (any_remote) {
+    if (!tr) fail("update_halo: no transport available to reach remote neighbours.");
+    if (device ? !tr->device_capable() : !tr->host_capable())
+      fail("update_halo: transport '", tr->name(), "' cannot move ", device ? "GPU" : "host", " memory.");
+  }
+  char* sbuf = send_bytes ? pool_.arena(0, send_bytes, device) : nullptr;
+  char* rbuf = recv_bytes ? pool_.arena(1, recv_bytes, device) : nullptr;
+  const int eb = fields[0].elem_bytes;
+  auto do_copies = [&](const std::vector<Copy2D>& cps) {
+    if (cps.empty()) return;
+    if (device) launch_copy2d(cps, eb, stream); else host_copy2d(cps, eb);
+  };
+  // 1. pack every non-zero-copy send region (one launch for all fields/directions)
+  std::vector<Copy2D> pack;
+  std::vector<P2POp> tsend, trecv;
+  std::vector<const char*> self_src(27 * fields.size(), nullptr);
+  for (const Msg& m : sends) {
+    const Face& fc = m.face;
+    char* dst = m.zero_copy ? fc.base : sbuf + m.off;
+    if (!m.zero_copy)
+      pack.push_back({fc.base, dst, fc.n_outer, fc.n_inner, fc.s_outer, fc.s_inner, fc.n_inner, 1});
+    if (m.peer == g.me) self_src[m.field * 27 + m.key] = dst;
+    else tsend.push_back({dst, fc.bytes, static_cast<int>(m.peer), static_cast<int>(m.field * 27 + m.key)});
+  }
+  do_copies(pack);
+  // 2. one communication phase for all remote messages
+  std::vector<Copy2D> unpack;
+  for (const Msg& m : recvs) {
+    const Face& fc = m.face;
+    const char* src;
+    if (m.peer == g.me) {
+      src = self_src[m.field * 27 + m.key];
+      if (!src) fail("one-phase exchange: missing self message (inconsistent peer table)");
+    } else {
+      char* dst = m.zero_copy ? fc.base : rbuf + m.off;
+      trecv.push_back({dst, fc.bytes, static_cast<int>(m.peer), static_cast<int>(m.field * 27 + m.key)});
+      src = dst;
+      if (m.zero_copy) continue;
+    }
+    unpack.push_back({src, fc.base, fc.n_outer, fc.n_inner, fc.n_inner, 1, fc.s_outer, fc.s_inner});
+  }
+  if (!tsend.empty() || !trecv.empty()) tr->exchange(trecv, tsend, device, stream);
+  // 3. unpack every receive region (disjoint: one launch)
   do_copies(unpack);
 }
 

@@ -45,13 +45,31 @@ struct Field {
   bool device = false;
 };
 
+// Index of direction v in {-1,0,1}^3 (13 = centre).
+inline int dir_key(int vx, int vy, int vz) { return (vx + 1) * 9 + (vy + 1) * 3 + (vz + 1); }
+
 struct GridInfo {
   int64_t me = 0, nprocs = 1;
   Int3 nxyz{1, 1, 1};
   Int3 overlaps{2, 2, 2};
   std::array<Int3, NNEIGHBORS> neighbors{{{PROC_NULL, PROC_NULL, PROC_NULL},
                                           {PROC_NULL, PROC_NULL, PROC_NULL}}};
+  // Rank at coords + disp*v for every direction v (dir_key order), PROC_NULL
+  // where it leaves a non-periodic grid. Needed by the one-phase exchange.
+  std::array<int64_t, 27> peers{};
+  bool has_peers = false;
 };
+
+// Halo update schedule.
+//   Sequential: x -> y -> z, faces only (the reference's algorithm).
+//   OnePhase:   all faces, edges and corners as independent messages in ONE
+//               pack launch / ONE communication group / ONE unpack launch;
+//               bitwise the same result (see halo.cpp). On a fully connected
+//               xGMI node every peer is one hop, so the 3 sequential latency
+//               phases collapse into 1 and messages to distinct peers use
+//               distinct links concurrently.
+//   Auto:       OnePhase when a remote peer exists, else Sequential.
+enum class HaloMode : int { Sequential = 0, OnePhase = 1, Auto = 2 };
 
 // A face (one plane of a field orthogonal to `dim`) as a strided 2-D region.
 struct Face {
@@ -60,6 +78,15 @@ struct Face {
   bool contiguous;
   size_t bytes;
 };
+
+// Half-open index box of a field.
+struct Region {
+  int64_t lo[3], hi[3];
+  int64_t count() const { return (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]); }
+};
+
+// A box with at most two non-singleton extents as a strided 2-D region.
+Face region_face(const Field& f, const Region& r);
 
 int64_t ol(const GridInfo& g, int dim, const Field& f);
 int64_t max_halo_elems(const Field& f);
@@ -78,6 +105,8 @@ class BufferPool {
   size_t nslots(bool device) const { return (device ? dev_ : host_).size(); }
   size_t capacity(size_t slot, bool device) const;
   bool allocated(bool device) const { return device ? dev_alloc_ : host_alloc_; }
+  // Grow-only send/recv arenas of the one-phase exchange.
+  char* arena(int which, size_t bytes, bool device);
   void free_all();
 
  private:
@@ -86,6 +115,7 @@ class BufferPool {
   void grow(Buf& b, size_t bytes, bool device);
   void release(Buf& b, bool device);
   std::vector<Slot> host_, dev_;
+  Buf arena_[2][2];  // [device][send/recv]
   bool host_alloc_ = false, dev_alloc_ = false;
 };
 
@@ -107,11 +137,20 @@ class HaloEngine {
   void exchange(const std::vector<Field>& fields, hipStream_t stream);
   // Only the dimension `dim` (0-based); used by tests and pipelined apps.
   void exchange_dim(const std::vector<Field>& fields, int dim, hipStream_t stream);
+  void set_mode(HaloMode m) { mode_ = m; }
+  HaloMode mode() const { return mode_; }
+  // Mode the next exchange of `fields` would use (Auto resolved).
+  HaloMode resolved_mode(const std::vector<Field>& fields) const;
+  int last_message_count() const { return last_msgs_; }
 
  private:
   void exchange_dim_impl(const std::vector<Field>& fields, int dim, bool device,
                          hipStream_t stream);
+  void exchange_onephase(const std::vector<Field>& fields, bool device, hipStream_t stream);
+  bool active(const Field& f, int d) const;
   GridInfo grid_;
+  HaloMode mode_ = HaloMode::Auto;
+  int last_msgs_ = 0;
   BufferPool pool_;
   std::shared_ptr<Transport> host_transport_, dev_transport_;
   hipEvent_t done_ = nullptr;

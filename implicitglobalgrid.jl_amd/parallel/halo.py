@@ -62,14 +62,52 @@ def field_tuple(t: torch.Tensor):
     return (t.data_ptr(), nd, size, stride, t.element_size(), bool(t.is_cuda))
 
 
+def peer_table(gg) -> list[int]:
+    """Rank at coords + disp*v for all 27 directions v (dir_key order: v in
+    {-1,0,1}^3, last component fastest), PROC_NULL off a non-periodic grid."""
+    dims = [int(d) for d in gg.dims]
+    out = []
+    for vx in (-1, 0, 1):
+        for vy in (-1, 0, 1):
+            for vz in (-1, 0, 1):
+                c, ok = [], True
+                for d, v in enumerate((vx, vy, vz)):
+                    x = int(gg.coords[d]) + int(gg.disp) * v
+                    if x < 0 or x >= dims[d]:
+                        if not gg.periods[d]:
+                            ok = False
+                            break
+                        x %= dims[d]
+                    c.append(x)
+                out.append(native.cart_rank(c, dims) if ok else PROC_NULL)
+    return out
+
+
 def _grid_info(gg) -> "native.GridInfo":
-    return native.GridInfo(int(gg.me), int(gg.nprocs), gg.nxyz.tolist(), gg.overlaps.tolist(), gg.neighbors.tolist())
+    return native.GridInfo(int(gg.me), int(gg.nprocs), gg.nxyz.tolist(), gg.overlaps.tolist(),
+                           gg.neighbors.tolist(), peer_table(gg))
+
+
+HALO_MODES = {"sequential": 0, "onephase": 1, "auto": 2}
+
+
+def set_halo_mode(mode: str) -> None:
+    """Select the exchange schedule: 'sequential' (x->y->z faces, the reference
+    algorithm), 'onephase' (faces+edges+corners in one phase) or 'auto'."""
+    _grid.check_initialized()
+    _engine.set_mode(HALO_MODES[mode])
+
+
+def halo_mode() -> str:
+    _grid.check_initialized()
+    return {v: k for k, v in HALO_MODES.items()}[_engine.mode]
 
 
 def _init_engine(gg) -> None:
     global _engine, _debug_sync
     _plans.clear()
     _engine = native.HaloEngine(_grid_info(gg))
+    _engine.set_mode(HALO_MODES[config.halo_mode()])
     _debug_sync = config.debug_sync()
     if gg.nprocs > 1:
         _engine.set_transport(gg.comm.host_transport(), False)
@@ -120,7 +158,10 @@ def enable_loopback(dims=(True, True, True)) -> None:
             gg.neighbors[:, d] = 0
     _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
     nb = gg.neighbors.tolist()
-    _engine.set_grid(native.GridInfo(1, 2, gg.nxyz.tolist(), gg.overlaps.tolist(), nb))
+    peers = [0 if all(dims[d] or c == 1 for d, c in enumerate((k // 9, (k // 3) % 3, k % 3))) else PROC_NULL
+             for k in range(27)]
+    peers[13] = 1
+    _engine.set_grid(native.GridInfo(1, 2, gg.nxyz.tolist(), gg.overlaps.tolist(), nb, peers))
     _engine.set_transport(_loopback_comm, True)
     _plans.clear()
 

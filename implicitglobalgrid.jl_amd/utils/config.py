@@ -65,6 +65,15 @@ def transport_choice(env: Mapping[str, str] | None = None) -> str:
     return t
 
 
+def halo_mode(env: Mapping[str, str] | None = None) -> str:
+    """``IGG_HALO_MODE``: ``auto`` (default) | ``sequential`` | ``onephase``."""
+    env = os.environ if env is None else env
+    m = env.get("IGG_HALO_MODE", "auto").strip().lower()
+    if m not in ("auto", "sequential", "onephase"):
+        raise ValueError(f"IGG_HALO_MODE must be auto, sequential or onephase (got {m!r})")
+    return m
+
+
 def debug_sync(env: Mapping[str, str] | None = None) -> bool:
     env = os.environ if env is None else env
     return env.get("IGG_DEBUG_SYNC", "0") not in ("", "0")

@@ -5,15 +5,17 @@ import pytest
 from tests._mp import run_ranks
 
 
+@pytest.mark.parametrize("mode", ["sequential", "onephase"])
 @pytest.mark.parametrize("nprocs,cfg", [
     (2, (7, 5, 6, 0, 0, 0)),
     (2, (7, 5, 6, 1, 1, 1)),   # dims 2x1x1 periodic: left == right neighbour
     (4, (7, 5, 6, 1, 0, 1)),
     (8, (7, 5, 6, 0, 0, 0)),   # 2x2x2
     (3, (7, 5, 6, 1, 1, 1)),
+    (8, (7, 5, 6, 1, 1, 1)),   # 2x2x2 periodic: every direction is a neighbour
 ])
-def test_halo_cpu_multirank(nprocs, cfg):
-    run_ranks(nprocs, "halo", "cpu", *cfg, "f64")
+def test_halo_cpu_multirank(nprocs, cfg, mode):
+    run_ranks(nprocs, "halo", "cpu", *cfg, "f64", env_extra={"IGG_HALO_MODE": mode})
 
 
 @pytest.mark.parametrize("nprocs,cfg,dims", [
@@ -23,6 +25,7 @@ def test_halo_cpu_multirank(nprocs, cfg):
 ])
 def test_halo_cpu_lowdim(nprocs, cfg, dims):
     run_ranks(nprocs, "halo", "cpu", *cfg, "f32", *dims)
+    run_ranks(nprocs, "halo", "cpu", *cfg, "f32", *dims, env_extra={"IGG_HALO_MODE": "sequential"})
 
 
 def test_halo_cpu_complex():
@@ -53,9 +56,10 @@ GPU_ENV = {"IGG_TRANSPORT": "staged"}
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sequential", "onephase"])
 @pytest.mark.parametrize("nprocs,cfg", [(2, (7, 5, 6, 1, 1, 1)), (8, (7, 5, 6, 0, 0, 0)), (4, (9, 6, 5, 1, 0, 1))])
-def test_halo_gpu_multirank_staged(nprocs, cfg):
-    run_ranks(nprocs, "halo", "gpu", *cfg, "f64", env_extra=GPU_ENV)
+def test_halo_gpu_multirank_staged(nprocs, cfg, mode):
+    run_ranks(nprocs, "halo", "gpu", *cfg, "f64", env_extra={**GPU_ENV, "IGG_HALO_MODE": mode})
 
 
 @pytest.mark.gpu

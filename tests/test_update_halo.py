@@ -194,15 +194,18 @@ def test_write_read_face(device):
 
 # --- 4. full halo updates ---------------------------------------------------------
 def _full(shape_or_tensor, grid_kw, dtype=torch.float64, complex_factor=None):
+    """Run the oracle with both exchange schedules (they must agree bitwise)."""
     igg.init_global_grid(*grid_kw.pop("n"), quiet=True, init_MPI=False, **grid_kw)
     gg = igg.get_global_grid()
     A = torch.zeros(shape_or_tensor, dtype=dtype)
     encode(A, complex_factor=complex_factor)
     ref = expected_after_halo(A, has_halo(A, gg), gg.neighbors.tolist())
-    X = zero_boundaries(A.clone())
-    assert not torch.equal(X, A)
-    igg.update_halo_(X)
-    assert torch.equal(X, ref)
+    for mode in ("sequential", "onephase"):
+        H.set_halo_mode(mode)
+        X = zero_boundaries(A.clone())
+        assert not torch.equal(X, A)
+        igg.update_halo_(X)
+        assert torch.equal(X, ref), mode
     igg.finalize_global_grid(finalize_MPI=False)
     return X, A
 
@@ -272,8 +275,10 @@ def test_other_element_types(dtype):
     assert torch.equal(X, A)
 
 
-def test_two_fields_simultaneously():
+@pytest.mark.parametrize("mode", ["sequential", "onephase"])
+def test_two_fields_simultaneously(mode):
     igg.init_global_grid(nx, ny, nz, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    H.set_halo_mode(mode)
     Vz = encode(torch.zeros(nx, ny, nz + 1, dtype=torch.float64))
     Vx = encode(torch.zeros(nx + 1, ny, nz, dtype=torch.float64))
     Vz_ref, Vx_ref = Vz.clone(), Vx.clone()
@@ -281,6 +286,18 @@ def test_two_fields_simultaneously():
     zero_boundaries(Vx)
     igg.update_halo_(Vz, Vx)
     assert torch.equal(Vz, Vz_ref) and torch.equal(Vx, Vx_ref)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_onephase_message_counts():
+    igg.init_global_grid(nx, ny, nz, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    H.set_halo_mode("onephase")
+    igg.update_halo_(torch.zeros(nx, ny, nz))
+    assert H.engine().last_message_count == 26  # 6 faces + 12 edges + 8 corners (all to self)
+    igg.update_halo_(torch.zeros(nx - 1, ny, nz))  # no halo in x: 4 faces + 4 edges
+    assert H.engine().last_message_count == 8
+    H.set_halo_mode("auto")
+    assert H.halo_mode() == "auto"
     igg.finalize_global_grid(finalize_MPI=False)
 
 
