@@ -42,8 +42,8 @@ def main():
     ap.add_argument("--dtype", default="float64")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--combos", default="0:18:-1,1:18:-1,4:18:-1,-1:18:-1,-2:18:-1,1:19:-1,-1:19:-1,1:0:-1",
-                    help="interior_rounds:halo_variant:halo_rounds list")
+    ap.add_argument("--combos", default="0:11:0:0,0:11:0:8,0:11:0:16,0:11:0:32,0:0:0:16",
+                    help="interior_rounds:halo_variant:halo_rounds:reserved_cus list")
     a = ap.parse_args()
     dtype = getattr(torch, a.dtype)
     n = a.n
@@ -54,12 +54,19 @@ def main():
     del m
     torch.cuda.empty_cache()
     H.enable_loopback()
-    mo = Diffusion3D(dtype=dtype, overlap=True)
     ms = Diffusion3D(dtype=dtype, overlap=False)
     combos = [tuple(int(x) for x in c.split(":")) for c in a.combos.split(",")]
-    res = {"plain": plain, "halo_only": [], "serial": [], "slabs_only": []}
+    models = {}
     for c in combos:
-        res[f"overlap_ir{c[0]}_hv{c[1]}_hr{c[2]}"] = []
+        if c[3] not in models:
+            models[c[3]] = Diffusion3D(dtype=dtype, overlap=True, reserve_cus=c[3])
+            models[c[3]].Cp = ms.Cp  # share inputs (memory)
+            models[c[3]].T, models[c[3]].T2 = ms.T.clone(), ms.T.clone()
+    mo = models[combos[0][3]]
+    res = {"plain": plain, "halo_only": [], "serial": []}
+    for c in combos:
+        res[f"overlap_ir{c[0]}_hv{c[1]}_hr{c[2]}_cu{c[3]}"] = []
+        res[f"slabs_hv{c[1]}_hr{c[2]}"] = []
 
     def slabs():
         from igg.ops import stencil as st
@@ -69,10 +76,10 @@ def main():
         res["halo_only"].append(timeit(lambda: igg.update_halo_(mo.T), a.reps, s))
         res["serial"].append(timeit(ms.step, a.reps, s))
         for c in combos:
-            mo.interior_rounds, mo.halo_variant, mo.halo_rounds = c
-            if not res["slabs_only"] or len(res["slabs_only"]) < a.rounds:
-                res["slabs_only"].append(timeit(slabs, a.reps, s))
-            res[f"overlap_ir{c[0]}_hv{c[1]}_hr{c[2]}"].append(timeit(mo.step, a.reps, s))
+            mo = models[c[3]]
+            mo.interior_rounds, mo.halo_variant, mo.halo_rounds = c[:3]
+            res[f"slabs_hv{c[1]}_hr{c[2]}"].append(timeit(slabs, a.reps, s))
+            res[f"overlap_ir{c[0]}_hv{c[1]}_hr{c[2]}_cu{c[3]}"].append(timeit(mo.step, a.reps, s))
     out = {k: round(statistics.median(v), 4) for k, v in res.items()}
     best = min((k for k in out if k.startswith("overlap")), key=lambda k: out[k])
     out["best_overlap"] = best

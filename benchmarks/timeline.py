@@ -30,7 +30,8 @@ def main():
     for r in rows:
         s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
         print(f"{s / 1e3:10.1f} {e / 1e3:10.1f} {(e - s) / 1e3:8.1f} us  q{r.get('Queue_Id', '?'):>3} "
-              f"grid={r.get('Grid_Size', '?'):>9} {short(r['Kernel_Name'])}")
+              f"grid={r.get('Grid_Size_X', r.get('Grid_Size', '?')):>9} wg={r.get('Workgroup_Size_X', '?'):>4} "
+              f"vgpr={r.get('VGPR_Count', '?'):>4} {short(r['Kernel_Name'])}")
 
 
 if __name__ == "__main__":

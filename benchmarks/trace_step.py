@@ -21,11 +21,12 @@ ap.add_argument("--hv", type=int, default=18)
 ap.add_argument("--hr", type=int, default=-1)
 ap.add_argument("--interior-first", type=int, default=0)
 ap.add_argument("--no-loopback", action="store_true")
+ap.add_argument("--cu", type=int, default=0)
 a = ap.parse_args()
 igg.init_global_grid(a.n, a.n, a.n, quiet=True)
 if not a.no_loopback:
     H.enable_loopback()
-m = Diffusion3D(dtype=torch.float64, interior_rounds=a.ir, halo_variant=a.hv, halo_rounds=a.hr)
+m = Diffusion3D(dtype=torch.float64, overlap=True, interior_rounds=a.ir, halo_variant=a.hv, halo_rounds=a.hr, reserve_cus=a.cu)
 m.interior_first = bool(a.interior_first)
 for _ in range(3):
     m.step()

@@ -156,6 +156,31 @@ PYBIND11_MODULE(_igg_native, m) {
     return py::bytes(out);
   });
   m.def("rccl_version", &rccl_version);
+  // Streams restricted to a subset of CUs (MI355X CU masking): the halo stream
+  // can own a few CUs so communication kernels (RCCL's spin on each other and
+  // need all their workgroups resident) never wait behind a compute kernel
+  // that fills every CU. Returns the hipStream_t as an integer.
+  m.def("stream_create_cu_mask", [](const std::vector<uint32_t>& mask, int priority) {
+    hipStream_t s = nullptr;
+    if (mask.empty()) {
+      IGG_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+    } else {
+      IGG_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
+    }
+    return reinterpret_cast<uintptr_t>(s);
+  }, py::arg("mask"), py::arg("priority") = 0);
+  m.def("stream_destroy", [](uintptr_t s) { IGG_HIP_CHECK(hipStreamDestroy(as_stream(s))); });
+  m.def("stream_get_cu_mask", [](uintptr_t s, int words) {
+    std::vector<uint32_t> m(static_cast<size_t>(words), 0u);
+    IGG_HIP_CHECK(hipExtStreamGetCUMask(as_stream(s), static_cast<uint32_t>(words), m.data()));
+    return m;
+  });
+  m.def("cu_count", []() {
+    int dev = 0, cus = 0;
+    IGG_HIP_CHECK(hipGetDevice(&dev));
+    IGG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    return cus;
+  });
   // Stream-ordered blocking copies for the host-staged transport: wait for all
   // prior work on `stream`, copy, wait again.
   m.def("memcpy_d2h_stream", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
@@ -318,6 +343,7 @@ PYBIND11_MODULE(_igg_native, m) {
     for (int i = 0; i < diffusion3d_num_variants(); ++i) v.push_back(diffusion3d_variant_name(i));
     return v;
   });
+  m.def("diffusion3d_variant_tile", &diffusion3d_variant_tile);
   m.def("stream_probe", [](int kind, uintptr_t out, uintptr_t a, uintptr_t b, int64_t n, int blocks,
                            uintptr_t stream) {
     launch_stream_probe(kind, reinterpret_cast<double*>(out), reinterpret_cast<const double*>(a),
@@ -341,11 +367,13 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
         py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
         py::arg("stream") = 0, py::arg("rounds") = 0);
-  m.def("split_boundary", [](const Int3& n, const std::array<bool, 3>& active, const Int3& w) {
+  m.def("split_boundary", [](const Int3& n, const std::array<std::array<bool, 2>, 3>& active,
+                             const Int3& w) {
     std::vector<Box> slabs;
     Box interior;
     int64_t nn[3] = {n[0], n[1], n[2]}, ww[3] = {w[0], w[1], w[2]};
-    bool aa[3] = {active[0], active[1], active[2]};
+    bool aa[3][2];
+    for (int d = 0; d < 3; ++d) { aa[d][0] = active[d][0]; aa[d][1] = active[d][1]; }
     split_boundary(nn, aa, ww, slabs, interior);
     std::vector<std::pair<Int3, Int3>> out;
     for (const Box& b : slabs) out.push_back(from_box(b));

@@ -37,6 +37,8 @@ struct DiffusionArgs {
 // Number of tuned kernel variants (see stencil_kernels.hip); variant 0 = default.
 int diffusion3d_num_variants();
 const char* diffusion3d_variant_name(int v);
+// Width (points along dim 2) of one workgroup tile of variant v.
+int diffusion3d_variant_tile(int v);
 // Grid sizing: number of full residency rounds per launch (<= 0: fixed 4096-block target).
 void diffusion3d_set_rounds(int rounds);
 int diffusion3d_get_rounds();
@@ -46,9 +48,9 @@ void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, i
 void host_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes);
 
 // Boundary-slab / interior decomposition of the inner box [1,n-1)^3.
-// Along each dim with `active[d]`, slabs of width w[d] at both ends are split
-// off (they hold the planes that update_halo sends). Returns {slabs, interior}.
-void split_boundary(const int64_t n[3], const bool active[3], const int64_t w[3],
+// At every side with `active[d][side]`, a slab of width w[d] is split off (it
+// holds the plane that update_halo sends to that side). Returns {slabs, interior}.
+void split_boundary(const int64_t n[3], const bool active[3][2], const int64_t w[3],
                     std::vector<Box>& slabs, Box& interior);
 
 }  // namespace igg

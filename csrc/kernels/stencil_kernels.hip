@@ -354,8 +354,13 @@ void for_each_table(const std::vector<Box>& boxes, int W, int TY, bool aligned, 
       bt.zt0[k] = zt0(bx);
       bt.ntz[k] = (bx.hi[2] - bt.zt0[k] + W - 1) / W;
       bt.nty[k] = (bx.hi[1] - bx.lo[1] + TY - 1) / TY;
-      // Equal-size chunks along the march (no short remainder chunk).
-      const int64_t nch = std::max<int64_t>(1, (len0 + ch_all - 1) / ch_all);
+      // Equal-size chunks along the march (no short remainder chunk). A thin
+      // box (few tiles, e.g. a one-row slab) gets shorter marches so it still
+      // spreads over >= ~256 workgroups instead of a few latency-bound ones.
+      const int64_t tiles_k = bt.ntz[k] * bt.nty[k];
+      const int64_t ch_box =
+          std::min<int64_t>(ch_all, std::max<int64_t>(4, (len0 * tiles_k + 255) / 256));
+      const int64_t nch = std::max<int64_t>(1, (len0 + ch_box - 1) / ch_box);
       const int64_t ch = (len0 + nch - 1) / nch;
       bt.ch[k] = ch;
       bt.start[k] = blocks;
@@ -445,6 +450,11 @@ void diffusion3d_set_rounds(int rounds) { g_rounds = rounds; }
 int diffusion3d_get_rounds() { return g_rounds; }
 const char* diffusion3d_variant_name(int v) {
   return (v >= 0 && v < NVARIANTS) ? VARIANTS[v].name : "invalid";
+}
+int diffusion3d_variant_tile(int v) {
+  if (v < 0 || v >= NVARIANTS) return 0;
+  const int bz = (v >= 12 && v <= 16) ? 2 : (v == 17 ? 4 : 1);
+  return 64 * VARIANTS[v].vz * bz;
 }
 
 void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, int variant,

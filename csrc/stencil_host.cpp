@@ -43,23 +43,28 @@ void host_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes) {
   }
 }
 
-void split_boundary(const int64_t n[3], const bool active[3], const int64_t w[3],
+void split_boundary(const int64_t n[3], const bool active[3][2], const int64_t w[3],
                     std::vector<Box>& slabs, Box& interior) {
-  // Inner region [1, n-1); the interior shrinks by w[d] at both ends of every
-  // active dim; slabs are the (disjoint) difference, peeled dim 0 first.
+  // Inner region [1, n-1); the interior shrinks by w[d] at every active side
+  // (a side with a neighbour); slabs are the (disjoint) difference, peeled
+  // dim 0 first.
   Box cur{{1, 1, 1}, {n[0] - 1, n[1] - 1, n[2] - 1}};
   slabs.clear();
   for (int d = 0; d < 3; ++d) {
-    if (!active[d]) continue;
     const int64_t len = cur.hi[d] - cur.lo[d];
     const int64_t wd = std::max<int64_t>(1, std::min<int64_t>(w[d], len / 2));
-    Box lo = cur, hi = cur;
-    lo.hi[d] = cur.lo[d] + wd;
-    hi.lo[d] = std::max(cur.hi[d] - wd, lo.hi[d]);
-    if (!lo.empty()) slabs.push_back(lo);
-    if (!hi.empty()) slabs.push_back(hi);
-    cur.lo[d] = lo.hi[d];
-    cur.hi[d] = hi.lo[d];
+    if (active[d][0]) {
+      Box lo = cur;
+      lo.hi[d] = cur.lo[d] + wd;
+      if (!lo.empty()) slabs.push_back(lo);
+      cur.lo[d] = lo.hi[d];
+    }
+    if (active[d][1]) {
+      Box hi = cur;
+      hi.lo[d] = std::max(cur.hi[d] - wd, cur.lo[d]);
+      if (!hi.empty()) slabs.push_back(hi);
+      cur.hi[d] = hi.lo[d];
+    }
   }
   interior = cur;
 }

@@ -33,8 +33,8 @@ from ..utils.tools import coords_g, nx_g, ny_g, nz_g
 class Diffusion3D:
     def __init__(self, *, dtype=torch.float64, device=None, lam: float = 1.0, cp_min: float = 1.0,
                  lx: float = 10.0, ly: float = 10.0, lz: float = 10.0, overlap: bool = False,
-                 slab_width=None, variant=None, halo_variant: int = 1, interior_rounds: int = 0,
-                 halo_rounds: int = -1):
+                 slab_width=None, variant=None, halo_variant=None, interior_rounds: int = 0,
+                 halo_rounds: int = 0, reserve_cus: int = 0):
         gg = _grid.global_grid()
         nx, ny, nz = (int(v) for v in gg.nxyz)
         if device is None:
@@ -47,10 +47,8 @@ class Diffusion3D:
         self.dz = lz / (nz_g() - 1)
         self.dt = min(self.dx ** 2, self.dy ** 2, self.dz ** 2) * cp_min / lam / 8.1
         self.variant = variant
-        # Overlap tuning: the send planes run with a low-register kernel variant
-        # (so their waves fit beside the interior kernel's) and the interior is
-        # launched with enough workgroups that blocks retire often, letting the
-        # high-priority halo stream's kernels (incl. RCCL's) get CUs.
+        # Overlap tuning knobs: kernel variant / grid rounds of the boundary
+        # slabs and grid rounds of the interior launch (see ops.stencil).
         self.halo_variant = halo_variant
         self.interior_rounds = interior_rounds
         self.halo_rounds = halo_rounds
@@ -66,30 +64,31 @@ class Diffusion3D:
         self.T = (100 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 3.0) / 2) ** 2)
                   + 50 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 1.5) / 2) ** 2)).to(dtype).contiguous()
         self.T2 = self.T.clone()
-        active = [bool((gg.neighbors[:, d] != -1).any()) for d in range(3)]
-        self.overlap = overlap and self.device.type == "cuda" and any(active)
+        sides = [[bool(gg.neighbors[0, d] != -1), bool(gg.neighbors[1, d] != -1)] for d in range(3)]
+        self.overlap = overlap and self.device.type == "cuda" and any(any(s) for s in sides)
         self.inner = [stencil.inner_box(shape)]
+        if self.overlap and self.variant is None:
+            self.variant = 11  # 128-point tiles: z-slabs stay one full tile wide
         if slab_width is None:
-            # Halo stream: only the planes update_halo sends (ol-1 and n-ol per
-            # active dim). The compute stream updates the WHOLE inner region, so
-            # those planes are written twice with bitwise-identical values (same
-            # kernel, same inputs): benign, and the interior keeps its aligned,
-            # full-efficiency tiling.
-            self.slabs = []
-            for d in range(3):
-                if not active[d]:
-                    continue
-                o = int(gg.overlaps[d])
-                for idx in (o - 1, shape[d] - o):
-                    lo, hi = [1, 1, 1], [s - 1 for s in shape]
-                    lo[d], hi[d] = idx, idx + 1
-                    self.slabs.append((tuple(lo), tuple(hi)))
-            self.interior = self.inner[0]
-        else:
-            self.slabs, self.interior = stencil.split_boundary(shape, active, slab_width)
+            # A slab at every side with a neighbour, just wide enough to hold
+            # the plane update_halo sends there (index ol-1 / n-ol) along dims
+            # 0/1; along the contiguous dim 2 (where a thin slab would waste
+            # whole cache lines per row) it is exactly one kernel tile wide, so
+            # both the slab launch and the interior launch run full tiles.
+            o = [int(v) for v in gg.overlaps]
+            v = self.variant if self.variant is not None else 0
+            tile = max(1, int(stencil.native.diffusion3d_variant_tile(v)))
+            slab_width = (max(1, o[0] - 1), max(1, o[1] - 1), max(o[2] - 1, tile - 1))
+        self.slabs, self.interior = stencil.split_boundary(shape, sides, slab_width)
+        self.compute_stream = None
         if self.overlap:
-            _least, greatest = torch.cuda.Stream.priority_range()
-            self.halo_stream = torch.cuda.Stream(device=self.device, priority=greatest)
+            if reserve_cus > 0:
+                from ..utils.streams import cu_partition
+
+                self.compute_stream, self.halo_stream = cu_partition(reserve_cus)
+            else:
+                _least, greatest = torch.cuda.Stream.priority_range()
+                self.halo_stream = torch.cuda.Stream(device=self.device, priority=greatest)
 
     def _kw(self, variant=None, rounds=0):
         return dict(lam=self.lam, dt=self.dt, dx=self.dx, dy=self.dy, dz=self.dz,
@@ -99,17 +98,24 @@ class Diffusion3D:
         """Advance one time step (T <- T2 after the update and halo exchange)."""
         T, T2, Cp = self.T, self.T2, self.Cp
         if self.overlap:
+            # 1. boundary slabs on the compute stream (full bandwidth, nothing
+            #    else running), 2. the halo exchange of T2 on the high-priority
+            #    stream after an event, 3. the interior concurrently on the
+            #    compute stream; slabs/interior/halo planes are disjoint.
             main = torch.cuda.current_stream()
             hs = self.halo_stream
+            cs = self.compute_stream or main
+            stencil.diffusion3d_(T2, T, Cp, boxes=self.slabs, **self._kw(self.halo_variant, self.halo_rounds))
             hs.wait_stream(main)
-            if self.interior_first:
-                stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw(None, self.interior_rounds))
+            if cs is not main:
+                cs.wait_stream(main)
             with torch.cuda.stream(hs):
-                stencil.diffusion3d_(T2, T, Cp, boxes=self.slabs, **self._kw(self.halo_variant, self.halo_rounds))
                 update_halo_(T2)
-            if not self.interior_first:
+            with torch.cuda.stream(cs):
                 stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw(None, self.interior_rounds))
             main.wait_stream(hs)
+            if cs is not main:
+                main.wait_stream(cs)
         else:
             stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
             update_halo_(T2)

@@ -113,6 +113,10 @@ def diffusion3d_reference(T, Cp, *, lam, dt, dx, dy, dz) -> torch.Tensor:
 
 
 def split_boundary(shape, active, widths):
-    """Boundary slabs + interior box of the inner region (see csrc/stencil_host.cpp)."""
-    slabs, interior = native.split_boundary(list(shape), list(active), list(widths))
+    """Boundary slabs + interior box of the inner region (see csrc/stencil_host.cpp).
+
+    ``active[d]`` is a bool (both sides) or a (left, right) pair of bools.
+    """
+    act = [[bool(a), bool(a)] if isinstance(a, (bool, int)) else [bool(a[0]), bool(a[1])] for a in active]
+    slabs, interior = native.split_boundary(list(shape), act, list(widths))
     return slabs, interior
