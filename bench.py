@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
     ap.add_argument("--loopback", action="store_true",
                     help="1 GPU: route all 6 faces through the RCCL remote path to itself (interior-rank emulation)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as a hipGraph (two captured steps per replay)")
     return ap.parse_args()
 
 
@@ -67,12 +69,13 @@ def main():
     model = Diffusion3D(dtype=dtype, overlap=args.overlap)
     for _ in range(args.warmup):
         model.step()
+    if args.graph:
+        model.capture()
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        model.step()
+    model.run(args.steps)
     torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
@@ -116,6 +119,7 @@ def main():
                 "stencil_variant": os.environ.get("IGG_STENCIL_VARIANT", "0"),
                 "finite": finite,
                 "loopback_emulation": bool(args.loopback),
+                "hip_graph": model.graph is not None,
             },
         }
         print(json.dumps(out), flush=True)

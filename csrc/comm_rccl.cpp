@@ -34,6 +34,7 @@ RcclComm::RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank)
   IGG_NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
   IGG_HIP_CHECK(hipMalloc(&scratch_, 256));
   IGG_HIP_CHECK(hipMemset(scratch_, 0, 256));
+  IGG_HIP_CHECK(hipDeviceSynchronize());
 }
 
 RcclComm::~RcclComm() {

@@ -100,10 +100,17 @@ char* BufferPool::arena(int which, size_t bytes, bool device) {
 
 void BufferPool::grow(Buf& b, size_t bytes, bool device) {
   if (b.bytes >= bytes) return;
+  if (frozen_)
+    fail("update_halo: halo buffers must grow during a hipGraph capture; run one eager "
+         "update_halo with the same fields before capturing.");
   release(b, device);
   if (device) {
     IGG_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&b.p), bytes));
     IGG_HIP_CHECK(hipMemset(b.p, 0, bytes));
+    // hipMemset runs on the null stream, which does not order against the
+    // non-blocking streams torch hands us: finish it before any pack kernel on
+    // the caller's stream can write the buffer (growth is rare).
+    IGG_HIP_CHECK(hipDeviceSynchronize());
   } else {
     b.p = static_cast<char*>(std::aligned_alloc(64, round_up(bytes, 64)));
     if (!b.p) fail("BufferPool: host allocation of ", bytes, " bytes failed");
@@ -174,12 +181,27 @@ HaloEngine::~HaloEngine() {
 void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) {
   if (fields.empty()) return;
   const bool device = fields[0].device;
+  bool capturing = false;
+  if (device) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    IGG_HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+    capturing = cs != hipStreamCaptureStatusNone;
+  }
+  // No allocation (hipMalloc / device-wide sync) may happen inside a capture.
+  struct Freeze {
+    BufferPool& p;
+    Freeze(BufferPool& q, bool on) : p(q) { p.set_frozen(on); }
+    ~Freeze() { p.set_frozen(false); }
+  } freeze(pool_, capturing);
   pool_.ensure(fields, device);
   if (device) {
     if (!done_) IGG_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
     // Buffers are shared across calls: order against the previous exchange if it
-    // ran on another stream.
-    if (have_event_ && last_stream_ != stream) IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_, 0));
+    // ran on another stream. Inside a graph capture the graph's own edges order
+    // the work (an event recorded outside the capture cannot be waited on), and
+    // replays are stream-ordered with eager exchanges by the caller.
+    if (!capturing && have_event_ && last_stream_ != stream)
+      IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_, 0));
   }
   if (resolved_mode(fields) == HaloMode::OnePhase) {
     exchange_onephase(fields, device, stream);
@@ -187,7 +209,7 @@ void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) 
     last_msgs_ = 0;
     for (int dim = 0; dim < NDIMS; ++dim) exchange_dim_impl(fields, dim, device, stream);
   }
-  if (device) {
+  if (device && !capturing) {
     IGG_HIP_CHECK(hipEventRecord(done_, stream));
     have_event_ = true;
     last_stream_ = stream;

@@ -108,8 +108,11 @@ class BufferPool {
   // Grow-only send/recv arenas of the one-phase exchange.
   char* arena(int which, size_t bytes, bool device);
   void free_all();
+  // While frozen (during a hipGraph capture) any growth is an error.
+  void set_frozen(bool f) { frozen_ = f; }
 
  private:
+  bool frozen_ = false;
   struct Buf { char* p = nullptr; size_t bytes = 0; };
   struct Slot { Buf send[NNEIGHBORS], recv[NNEIGHBORS]; };
   void grow(Buf& b, size_t bytes, bool device);

@@ -1,9 +1,12 @@
 // Batched strided 2-D copy kernel for gfx950 (pack / unpack / self-periodic /
-// gather reorder). One launch covers every face of every field of one
-// dimension, both sides: the reference launches one (1,32,1)/(32,1,1)-thread
-// kernel per field and side (src/update_halo.jl:497-501), i.e. 32-lane groups
-// that waste half of every 64-lane CDNA wavefront. Here: 256-thread blocks
-// (4 full waves), 4 elements per thread, block->copy mapping by prefix sums.
+// one-phase messages). One launch covers every face (and edge/corner message)
+// of every field: the reference launches one (1,32,1)/(32,1,1)-thread kernel per
+// field and side (src/update_halo.jl:497-501), i.e. 32-lane groups that waste
+// half of every 64-lane CDNA wavefront. Here: 256-thread workgroups (4 full
+// waves); a workgroup copies one CHUNK of one row (the inner, fastest-varying
+// extent of the region), so the per-element index math is a single multiply-add
+// and the block->(copy, row, chunk) decode is scalar (once per workgroup).
+// Rows with unit stride on both sides move 4 elements per lane in flight.
 #include <hip/hip_runtime.h>
 
 #include "igg/copy.hpp"
@@ -12,8 +15,8 @@ namespace igg {
 namespace {
 
 constexpr int BLOCK = 256;
-constexpr int EPT = 4;  // elements per thread
-constexpr int64_t ELEMS_PER_BLOCK = BLOCK * EPT;
+constexpr int EPT = 4;                         // elements per thread per chunk
+constexpr int64_t CHUNK = BLOCK * EPT;         // elements of a row per workgroup
 
 struct alignas(16) B16 { uint64_t x, y; };
 
@@ -24,49 +27,72 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
   // Wave-uniform scan over <= MAX_BATCH prefix sums (scalar loads from kernarg).
   while (c + 1 < batch.n && b >= batch.block_start[c + 1]) ++c;
   const Copy2D& cp = batch.c[c];
-  const int64_t total = cp.n_outer * cp.n_inner;
-  const int64_t base = (b - batch.block_start[c]) * ELEMS_PER_BLOCK + threadIdx.x;
-  const T* __restrict__ src = reinterpret_cast<const T*>(cp.src);
-  T* __restrict__ dst = reinterpret_cast<T*>(cp.dst);
+  const int64_t local = b - batch.block_start[c];
+  const int64_t nchunks = (cp.n_inner + CHUNK - 1) / CHUNK;
+  const int64_t o = local / nchunks;              // row (outer index)
+  const int64_t i0 = (local - o * nchunks) * CHUNK;
+  const T* __restrict__ src = reinterpret_cast<const T*>(cp.src) + o * cp.src_so;
+  T* __restrict__ dst = reinterpret_cast<T*>(cp.dst) + o * cp.dst_so;
+  const int64_t n = cp.n_inner;
   T v[EPT];
-  int64_t doff[EPT];
-  bool ok[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
-    const int64_t e = base + k * BLOCK;
-    ok[k] = e < total;
-    const int64_t o = ok[k] ? e / cp.n_inner : 0;
-    const int64_t i = ok[k] ? e - o * cp.n_inner : 0;
-    if (ok[k]) v[k] = src[o * cp.src_so + i * cp.src_si];
-    doff[k] = o * cp.dst_so + i * cp.dst_si;
+    const int64_t i = i0 + k * BLOCK + threadIdx.x;
+    if (i < n) v[k] = src[i * cp.src_si];
   }
 #pragma unroll
-  for (int k = 0; k < EPT; ++k)
-    if (ok[k]) dst[doff[k]] = v[k];
+  for (int k = 0; k < EPT; ++k) {
+    const int64_t i = i0 + k * BLOCK + threadIdx.x;
+    if (i < n) dst[i * cp.dst_si] = v[k];
+  }
+}
+
+// Copies whose rows are short (n_inner < 64, e.g. a face whose inner extent is
+// tiny or an edge/corner message) are flattened: one element per lane.
+template <typename T>
+__global__ void __launch_bounds__(BLOCK) copy2d_flat_kernel(const CopyBatch batch) {
+  const int64_t b = blockIdx.x;
+  int c = 0;
+  while (c + 1 < batch.n && b >= batch.block_start[c + 1]) ++c;
+  const Copy2D& cp = batch.c[c];
+  const int64_t e = (b - batch.block_start[c]) * BLOCK + threadIdx.x;
+  if (e >= cp.n_outer * cp.n_inner) return;
+  const int64_t o = e / cp.n_inner, i = e - o * cp.n_inner;
+  reinterpret_cast<T*>(cp.dst)[o * cp.dst_so + i * cp.dst_si] =
+      reinterpret_cast<const T*>(cp.src)[o * cp.src_so + i * cp.src_si];
 }
 
 template <typename T>
 void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream) {
-  size_t pos = 0;
-  while (pos < copies.size()) {
-    CopyBatch batch{};
-    batch.n = 0;
-    int64_t blocks = 0;
-    while (pos < copies.size() && batch.n < MAX_BATCH) {
-      const Copy2D& c = copies[pos++];
-      const int64_t total = c.n_outer * c.n_inner;
-      if (total <= 0) continue;
-      batch.c[batch.n] = c;
+  for (int flat = 0; flat < 2; ++flat) {
+    size_t pos = 0;
+    while (pos < copies.size()) {
+      CopyBatch batch{};
+      batch.n = 0;
+      int64_t blocks = 0;
+      while (pos < copies.size() && batch.n < MAX_BATCH) {
+        const Copy2D& c = copies[pos++];
+        const int64_t total = c.n_outer * c.n_inner;
+        if (total <= 0) continue;
+        const bool is_flat = c.n_inner < 64;
+        if (is_flat != (flat == 1)) continue;
+        batch.c[batch.n] = c;
+        batch.block_start[batch.n] = blocks;
+        blocks += is_flat ? (total + BLOCK - 1) / BLOCK
+                          : c.n_outer * ((c.n_inner + CHUNK - 1) / CHUNK);
+        ++batch.n;
+      }
+      if (batch.n == 0) continue;
       batch.block_start[batch.n] = blocks;
-      blocks += (total + ELEMS_PER_BLOCK - 1) / ELEMS_PER_BLOCK;
-      ++batch.n;
+      if (blocks > 0x7fffffffLL) fail("launch_copy2d: too many blocks (", blocks, ")");
+      if (flat)
+        hipLaunchKernelGGL(copy2d_flat_kernel<T>, dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
+                           stream, batch);
+      else
+        hipLaunchKernelGGL(copy2d_batch_kernel<T>, dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
+                           stream, batch);
+      IGG_HIP_CHECK(hipGetLastError());
     }
-    if (batch.n == 0) continue;
-    batch.block_start[batch.n] = blocks;
-    if (blocks > 0x7fffffffLL) fail("launch_copy2d: too many blocks (", blocks, ")");
-    hipLaunchKernelGGL(copy2d_batch_kernel<T>, dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
-                       stream, batch);
-    IGG_HIP_CHECK(hipGetLastError());
   }
 }
 

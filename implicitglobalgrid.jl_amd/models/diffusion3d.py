@@ -26,7 +26,7 @@ import torch
 from .. import parallel  # noqa: F401
 from ..ops import stencil
 from ..parallel import grid as _grid
-from ..parallel.halo import update_halo_
+from ..parallel.halo import register_graph, update_halo_
 from ..utils.tools import coords_g, nx_g, ny_g, nz_g
 
 
@@ -53,6 +53,8 @@ class Diffusion3D:
         self.interior_rounds = interior_rounds
         self.halo_rounds = halo_rounds
         self.interior_first = False
+        self.graph = None
+        self._warm = False
         shape = (nx, ny, nz)
         probe = torch.empty(shape, device="meta")  # sizes only, for coords_g
         kw = dict(dtype=torch.float64, device=self.device)
@@ -120,8 +122,37 @@ class Diffusion3D:
             stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
             update_halo_(T2)
         self.T, self.T2 = T2, T
+        self._warm = True
+
+    def capture(self) -> None:
+        """Record two time steps (T -> T2 -> T) in a hipGraph for ``run``.
+
+        A step is a chain of short launches (stencil, pack, RCCL group, unpack
+        per dimension) whose gaps are host launch latency; replaying a graph
+        removes that latency. Two steps are captured so the ping-pong buffers
+        are back in their roles after every replay. Needs one eager step first
+        (halo buffers, plan cache and kernel variant are set up outside the
+        capture); ``capture`` performs that step itself if none ran yet.
+        """
+        if self.device.type != "cuda":
+            raise RuntimeError("Diffusion3D.capture: hipGraphs need a GPU model")
+        if not self._warm:
+            self.step()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            self.step()
+            self.step()
+        torch.cuda.synchronize()
+        register_graph(g)
+        self.graph = g
 
     def run(self, nt: int) -> None:
+        """Advance ``nt`` steps (by graph replays of two steps if captured)."""
+        if self.graph is not None:
+            for _ in range(nt // 2):
+                self.graph.replay()
+            nt %= 2
         for _ in range(nt):
             self.step()
 

@@ -26,6 +26,28 @@ _plans: dict = {}
 _MAX_PLANS = 512
 _buf_dtype = {False: None, True: None}
 _debug_sync = False
+_graphs: list = []  # weakrefs to hipGraphs that captured update_halo_
+
+
+def register_graph(g) -> None:
+    """Record a captured ``torch.cuda.CUDAGraph`` whose nodes use the halo
+    buffers / RCCL communicator, so freeing those resets the graph first (a
+    replay then fails loudly instead of touching freed memory, and RCCL's
+    communicator is never destroyed under a live graph, which hangs)."""
+    import weakref
+
+    _graphs[:] = [r for r in _graphs if r() is not None]
+    _graphs.append(weakref.ref(g))
+
+
+def _release_graphs() -> None:
+    live = [r() for r in _graphs]
+    _graphs.clear()
+    if any(g is not None for g in live):
+        torch.cuda.synchronize()
+    for g in live:
+        if g is not None:
+            g.reset()
 
 
 def _join(items) -> str:
@@ -117,6 +139,7 @@ def _init_engine(gg) -> None:
 
 def _drop_engine() -> None:
     global _engine, _loopback_comm
+    _release_graphs()
     _plans.clear()
     if _engine is not None:
         _engine.pool_free()
@@ -252,7 +275,7 @@ def update_halo_(*fields) -> None:
     stream = torch.cuda.current_stream().cuda_stream if device else 0
     _engine.exchange_set(fs, stream)
     _buf_dtype[device] = dtype
-    if _debug_sync and device:
+    if _debug_sync and device and not torch.cuda.is_current_stream_capturing():
         native.stream_synchronize(stream)
 
 
@@ -299,6 +322,7 @@ def allocate_bufs(*fields) -> None:
 
 
 def free_update_halo_buffers() -> None:
+    _release_graphs()
     if _engine is not None:
         native.device_synchronize() if _engine.pool_allocated(True) else None
         _engine.pool_free()

@@ -103,7 +103,9 @@ def scenario_diffusion(dev, nx, ny, nz, steps, overlap):
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, quiet=True, select_device=False,
                                                           device_type="AMDGPU" if dev == "gpu" else "auto")
     gg = igg.get_global_grid()
-    m = Diffusion3D(dtype=torch.float64, device=device, overlap=bool(int(overlap)))
+    v = os.environ.get("IGG_TEST_VARIANT")
+    m = Diffusion3D(dtype=torch.float64, device=device, overlap=bool(int(overlap)),
+                    variant=None if v is None else int(v))
     m.run(steps)
     loc = m.T.cpu()
     # global reference: same physics on the implicit global grid, one array

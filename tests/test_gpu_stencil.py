@@ -1,0 +1,69 @@
+"""Every HIP diffusion kernel variant on arbitrary sub-boxes (the boundary slabs
+and interior boxes of the overlapped step) against the plain-PyTorch fp64
+reference of the reference example's update (diffusion3D_multigpu_CuArrays_novis.jl).
+Cells outside the boxes must stay untouched."""
+import itertools
+
+import pytest
+import torch
+
+import igg  # noqa: F401
+from igg.ops import stencil
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(lam=1.0, dt=0.01, dx=0.3, dy=0.25, dz=0.2)
+
+
+def _fields(shape, dtype, gpu):
+    g = torch.Generator().manual_seed(1)
+    T = torch.rand(shape, generator=g, dtype=torch.float64)
+    Cp = 1 + torch.rand(shape, generator=g, dtype=torch.float64)
+    return T, Cp, T.to(dtype).to(gpu), Cp.to(dtype).to(gpu)
+
+
+def _run_boxes(shape, boxes, variant, dtype, gpu):
+    T, Cp, Tg, Cpg = _fields(shape, dtype, gpu)
+    sentinel = -7.0
+    T2g = torch.full(shape, sentinel, dtype=dtype, device=gpu)
+    stencil.diffusion3d_(T2g, Tg, Cpg, boxes=boxes, variant=variant, **KW)
+    if T2g.is_cuda:
+        torch.cuda.synchronize()
+    ref = stencil.diffusion3d_reference(Tg.double().cpu(), Cpg.double().cpu(), **KW)
+    got = T2g.double().cpu()
+    mask = torch.zeros(shape, dtype=torch.bool)
+    for lo, hi in boxes:
+        mask[lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]] = True
+    tol = 1e-12 if dtype == torch.float64 else 1e-5
+    assert (got[~mask] == sentinel).all(), "kernel wrote outside its boxes"
+    err = (got[mask] - ref[mask]).abs().max().item() if mask.any() else 0.0
+    return err, tol
+
+
+@pytest.mark.parametrize("variant", range(len(stencil.variants())))
+def test_variant_full_inner_box(gpu, variant):
+    for shape in [(24, 20, 18), (37, 33, 131), (9, 70, 5)]:
+        err, tol = _run_boxes(shape, [stencil.inner_box(shape)], variant, torch.float64, gpu)
+        assert err < tol, (shape, err)
+
+
+@pytest.mark.parametrize("variant", range(len(stencil.variants())))
+def test_variant_split_boxes(gpu, variant):
+    """Slabs + interior of split_boundary for one-sided and two-sided neighbours."""
+    shape = (24, 20, 18)
+    for act, w in itertools.product([[(0, 1), (1, 0), (0, 1)], [(1, 1), (1, 1), (1, 1)], [(1, 0), (0, 0), (1, 1)]],
+                                    [(1, 1, 1), (1, 1, 127), (2, 3, 63)]):
+        slabs, interior = stencil.split_boundary(shape, act, w)
+        for boxes in (slabs, [interior], list(slabs) + [interior]):
+            boxes = [b for b in boxes if all(h > l for l, h in zip(b[0], b[1]))]
+            if not boxes:
+                continue
+            err, tol = _run_boxes(shape, boxes, variant, torch.float64, gpu)
+            assert err < tol, (act, w, boxes, err)
+
+
+@pytest.mark.parametrize("variant", [0, 11])
+def test_variant_float32(gpu, variant):
+    shape = (40, 36, 70)
+    err, tol = _run_boxes(shape, [stencil.inner_box(shape)], variant, torch.float32, gpu)
+    assert err < tol
