@@ -13,6 +13,7 @@
 #include "igg/copy.hpp"
 #include "igg/gather.hpp"
 #include "igg/halo.hpp"
+#include "igg/ipc.hpp"
 #include "igg/stencil.hpp"
 #include "igg/topology.hpp"
 
@@ -156,6 +157,27 @@ PYBIND11_MODULE(_igg_native, m) {
     return py::bytes(out);
   });
   m.def("rccl_version", &rccl_version);
+
+  // --- intra-node peer memory (put transport primitives)
+  m.def("ipc_malloc", [](size_t bytes, int kind) {
+    return reinterpret_cast<uintptr_t>(ipc_malloc(bytes, static_cast<MemKind>(kind)));
+  });
+  m.def("ipc_free", [](uintptr_t p) { ipc_free(reinterpret_cast<void*>(p)); });
+  m.def("ipc_get_handle", [](uintptr_t p) { return py::bytes(ipc_get_handle(reinterpret_cast<void*>(p))); });
+  m.def("ipc_open", [](const std::string& h) { return reinterpret_cast<uintptr_t>(ipc_open(h)); });
+  m.def("ipc_close", [](uintptr_t p) { ipc_close(reinterpret_cast<void*>(p)); });
+  m.def("stream_write_u64", [](uintptr_t s, uintptr_t p, uint64_t v) {
+    stream_write_u64(as_stream(s), reinterpret_cast<void*>(p), v);
+  });
+  m.def("stream_wait_u64_geq", [](uintptr_t s, uintptr_t p, uint64_t v) {
+    stream_wait_u64_geq(as_stream(s), reinterpret_cast<void*>(p), v);
+  });
+  m.def("can_stream_wait_value", &can_stream_wait_value);
+  m.def("read_u64", [](uintptr_t p) {
+    uint64_t v = 0;
+    IGG_HIP_CHECK(hipMemcpy(&v, reinterpret_cast<void*>(p), 8, hipMemcpyDeviceToHost));
+    return v;
+  });
   // Streams restricted to a subset of CUs (MI355X CU masking): the halo stream
   // can own a few CUs so communication kernels (RCCL's spin on each other and
   // need all their workgroups resident) never wait behind a compute kernel
@@ -246,6 +268,33 @@ PYBIND11_MODULE(_igg_native, m) {
   py::class_<PyTransport, Transport, std::shared_ptr<PyTransport>>(m, "PyTransport")
       .def(py::init<py::function, bool, bool, std::string>(), py::arg("fn"), py::arg("host"),
            py::arg("device"), py::arg("name"));
+  py::class_<PeerMesh, std::shared_ptr<PeerMesh>>(m, "PeerMesh")
+      .def(py::init([](int rank, int nranks, py::function allgather) {
+             // Called from C++ (GIL held: exchanges run with the GIL).
+             PeerMesh::AllGather ag = [allgather](const std::string& mine) {
+               py::gil_scoped_acquire gil;
+               py::list out = allgather(py::bytes(mine));
+               std::vector<std::string> v;
+               for (auto h : out) v.push_back(h.cast<std::string>());
+               return v;
+             };
+             return std::make_shared<PeerMesh>(rank, nranks, ag);
+           }),
+           py::arg("rank"), py::arg("nranks"), py::arg("allgather"))
+      .def_property_readonly("rank", &PeerMesh::rank)
+      .def_property_readonly("nranks", &PeerMesh::nranks)
+      .def_property_readonly("arena_bytes", &PeerMesh::arena_bytes)
+      .def_property_readonly("epoch", &PeerMesh::epoch)
+      .def("flag", [](const PeerMesh& m, int idx) {
+        if (idx < 0 || idx >= PeerMesh::NFLAGS) fail("PeerMesh.flag: index out of range");
+        uint64_t v = 0;
+        IGG_HIP_CHECK(hipMemcpy(&v, m.flags(m.rank()) + idx, 8, hipMemcpyDeviceToHost));
+        return v;
+      })
+      .def("close", &PeerMesh::close);
+  py::class_<PutTransport, Transport, std::shared_ptr<PutTransport>>(m, "PutTransport")
+      .def(py::init<std::shared_ptr<PeerMesh>>(), py::arg("mesh"))
+      .def_property_readonly("mesh", &PutTransport::mesh_ptr);
   py::class_<RcclComm, Transport, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def_static("unique_id", []() {
         auto v = RcclComm::unique_id();

@@ -1,7 +1,11 @@
 // Halo exchange engine (see include/igg/halo.hpp for the behavioural contract).
 #include "igg/halo.hpp"
+#include "igg/ipc.hpp"
+
+#include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <limits>
 
@@ -203,7 +207,13 @@ void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) 
     if (!capturing && have_event_ && last_stream_ != stream)
       IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_, 0));
   }
-  if (resolved_mode(fields) == HaloMode::OnePhase) {
+  auto* put = device ? dynamic_cast<PutTransport*>(dev_transport_.get()) : nullptr;
+  if (put) {
+    // Stream flag values are baked into a captured graph, but every exchange
+    // needs a new epoch: the put transport cannot be replayed from a graph.
+    if (capturing) fail("update_halo: the 'put' transport cannot be captured in a hipGraph.");
+    exchange_put(fields, stream, put->mesh());
+  } else if (resolved_mode(fields) == HaloMode::OnePhase) {
     exchange_onephase(fields, device, stream);
   } else {
     last_msgs_ = 0;
@@ -351,6 +361,124 @@ struct Msg {
 constexpr size_t MSG_ALIGN = 256;
 }  // namespace
 
+bool HaloEngine::dir_regions(const Field& f, int key, Region& rr, Region& sr) const {
+  const GridInfo& g = grid_;
+  const int u[3] = {key / 9 - 1, (key / 3) % 3 - 1, key % 3 - 1};  // receiver-side direction
+  for (int d = 0; d < NDIMS; ++d) {
+    const int64_t n = f.size[d];
+    if (u[d] != 0) {
+      if (!active(f, d)) return false;
+      const int64_t o = ol(g, d, f);
+      // receive into my halo plane on side u_d; the matching send (direction
+      // -u) reads my send plane on side -u_d.
+      rr.lo[d] = u[d] < 0 ? 0 : n - 1;
+      sr.lo[d] = u[d] < 0 ? n - o : o - 1;
+      rr.hi[d] = rr.lo[d] + 1;
+      sr.hi[d] = sr.lo[d] + 1;
+    } else {
+      // Exclude the halo planes that another message fills (neighbour exists).
+      const bool act = active(f, d);
+      rr.lo[d] = sr.lo[d] = (act && g.neighbors[0][d] != PROC_NULL) ? 1 : 0;
+      rr.hi[d] = sr.hi[d] = (act && g.neighbors[1][d] != PROC_NULL) ? n - 1 : n;
+    }
+  }
+  return rr.count() > 0;
+}
+
+void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stream, PeerMesh& mesh) {
+  const GridInfo& g = grid_;
+  if (!g.has_peers) fail("the put transport needs the peer table (GridInfo.peers)");
+  const size_t nf = fields.size();
+  const int eb = fields[0].elem_bytes;
+  // Arena slot of (key, field): a function of the field shapes only, so every
+  // rank computes the same layout for the same call.
+  std::vector<size_t> slot(27 * nf, 0);
+  size_t per = 0;
+  for (int key = 0; key < 27; ++key) {
+    if (key == 13) continue;
+    const int u[3] = {key / 9 - 1, (key / 3) % 3 - 1, key % 3 - 1};
+    for (size_t i = 0; i < nf; ++i) {
+      int64_t elems = 1;
+      for (int d = 0; d < NDIMS; ++d) elems *= u[d] != 0 ? 1 : fields[i].size[d];
+      slot[key * nf + i] = per;
+      per += static_cast<size_t>(round_up(elems * eb, static_cast<int64_t>(MSG_ALIGN)));
+    }
+  }
+  mesh.ensure_arena(2 * per);  // collective, grow-only
+  const uint64_t k = mesh.next_epoch();
+  // Fixed halves per parity (independent of this call's layout), so messages
+  // of exchange k-1 and k never share bytes whatever fields either carried.
+  const size_t pbase = (k & 1) * (mesh.arena_bytes() / 2);
+  const int me = mesh.rank();
+  std::vector<Copy2D> put, unpack;
+  std::vector<int> out_keys, in_keys;
+  for (int key = 0; key < 27; ++key) {
+    if (key == 13) continue;
+    const int64_t from = g.peers[key], to = g.peers[26 - key];
+    bool any_in = false, any_out = false;
+    for (size_t i = 0; i < nf; ++i) {
+      const Field& f = fields[i];
+      Region rr{}, sr{};
+      if (!dir_regions(f, key, rr, sr)) continue;
+      const size_t off = pbase + slot[key * nf + i];
+      if (to != PROC_NULL) {
+        const Face sf = region_face(f, sr);
+        put.push_back({sf.base, mesh.arena(static_cast<int>(to)) + off, sf.n_outer, sf.n_inner, sf.s_outer,
+                       sf.s_inner, sf.n_inner, 1});
+        any_out = true;
+      }
+      if (from != PROC_NULL) {
+        const Face rf = region_face(f, rr);
+        unpack.push_back({mesh.arena(me) + off, rf.base, rf.n_outer, rf.n_inner, rf.n_inner, 1, rf.s_outer,
+                          rf.s_inner});
+        any_in = true;
+      }
+    }
+    if (any_out) out_keys.push_back(key);
+    if (any_in) in_keys.push_back(key);
+  }
+  last_msgs_ = static_cast<int>(put.size());
+  // 1. each receiver has finished unpacking exchange k-2 (the last one that
+  //    used this parity of its arena); slot = my direction towards it.
+  if (k > 2)
+    for (int key : out_keys) stream_wait_u64_geq(stream, mesh.flags(me) + PeerMesh::FREED + (26 - key), k - 2);
+  // 2. pack straight into the receivers' arenas (stores over xGMI), 3. signal
+  launch_copy2d(put, eb, stream, /*system_fence=*/true);
+  for (int key : out_keys)
+    stream_write_u64(stream, mesh.flags(static_cast<int>(g.peers[26 - key])) + PeerMesh::ARRIVED + key, k);
+  // 4. wait for my messages, unpack them, then tell EVERY neighbour that my
+  //    arena is consumed up to epoch k (also those that sent nothing now:
+  //    they may send next time, into a layout that overlaps this one).
+  for (int key : in_keys) stream_wait_u64_geq(stream, mesh.flags(me) + PeerMesh::ARRIVED + key, k);
+  launch_copy2d(unpack, eb, stream);
+  for (int key = 0; key < 27; ++key)
+    if (key != 13 && g.peers[key] != PROC_NULL)
+      stream_write_u64(stream, mesh.flags(static_cast<int>(g.peers[key])) + PeerMesh::FREED + (26 - key), k);
+  static const bool debug = std::getenv("IGG_PUT_DEBUG") != nullptr;
+  if (debug) {
+    // Bounded drain with a report of the flags this rank waits on.
+    std::fprintf(stderr, "[put rank %d] epoch %llu: %zu puts, %zu unpacks, out keys %zu, in keys %zu\n", me,
+                 static_cast<unsigned long long>(k), put.size(), unpack.size(), out_keys.size(), in_keys.size());
+    for (int it = 0; it < 5000 && hipStreamQuery(stream) == hipErrorNotReady; ++it) usleep(1000);
+    if (hipStreamQuery(stream) == hipErrorNotReady) {
+      hipStream_t side;
+      IGG_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+      uint64_t fl[PeerMesh::NFLAGS];
+      IGG_HIP_CHECK(hipMemcpyAsync(fl, mesh.flags(me), sizeof(fl), hipMemcpyDeviceToHost, side));
+      IGG_HIP_CHECK(hipStreamSynchronize(side));
+      for (int key : in_keys)
+        std::fprintf(stderr, "[put rank %d] STUCK epoch %llu: arrived[%d]=%llu from %lld\n", me,
+                     static_cast<unsigned long long>(k), key, static_cast<unsigned long long>(fl[key]),
+                     static_cast<long long>(g.peers[key]));
+      for (int key : out_keys)
+        std::fprintf(stderr, "[put rank %d]   freed[%d]=%llu (to %lld)\n", me, 26 - key,
+                     static_cast<unsigned long long>(fl[PeerMesh::FREED + 26 - key]),
+                     static_cast<long long>(g.peers[26 - key]));
+      fail("put transport: exchange did not complete within 5 s (IGG_PUT_DEBUG)");
+    }
+  }
+}
+
 void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device,
                                    hipStream_t stream) {
   const GridInfo& g = grid_;
@@ -365,40 +493,39 @@ void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device
     const int64_t to = g.peers[26 - key];              // I send in direction -u
     for (size_t i = 0; i < fields.size(); ++i) {
       const Field& f = fields[i];
-      bool ok = true;
       Region rr{}, sr{};
-      for (int d = 0; d < NDIMS && ok; ++d) {
-        const int64_t n = f.size[d];
-        if (u[d] != 0) {
-          if (!active(f, d)) { ok = false; break; }
-          const int64_t o = ol(g, d, f);
-          // receive into my halo plane on side u_d; the matching send (direction
-          // -u) reads my send plane on side -u_d.
-          rr.lo[d] = u[d] < 0 ? 0 : n - 1;
-          sr.lo[d] = u[d] < 0 ? n - o : o - 1;
-        } else {
-          const bool act = active(f, d);
-          rr.lo[d] = (act && g.neighbors[0][d] != PROC_NULL) ? 1 : 0;
-          const int64_t hi = (act && g.neighbors[1][d] != PROC_NULL) ? n - 1 : n;
-          rr.hi[d] = hi;
-          sr.lo[d] = rr.lo[d];
-          sr.hi[d] = hi;
-          continue;
-        }
-        rr.hi[d] = rr.lo[d] + 1;
-        sr.hi[d] = sr.lo[d] + 1;
-      }
-      if (!ok || rr.count() <= 0) continue;
+      if (!dir_regions(f, key, rr, sr)) continue;
+      // A face (one non-zero component) whose FULL plane is contiguous (the
+      // outermost dim of a C-order field) travels as that whole plane, zero-copy
+      // on both sides. The rows it carries beyond the region (halo rows of the
+      // other dims) are stale, but exactly those rows arrive as edge/corner
+      // messages, which always go through the receive arena and are unpacked
+      // after the RCCL group has completed — so they overwrite the stale rows
+      // deterministically. Edge/corner receives are therefore never zero-copy.
+      const int nnz = (u[0] != 0) + (u[1] != 0) + (u[2] != 0);
+      Region rfull = rr, sfull = sr;
+      for (int d = 0; d < NDIMS; ++d)
+        if (u[d] == 0) { rfull.lo[d] = sfull.lo[d] = 0; rfull.hi[d] = sfull.hi[d] = f.size[d]; }
       if (from != PROC_NULL) {
         Msg m{i, key, from, region_face(f, rr), 0, false};
-        m.zero_copy = m.face.contiguous && from != g.me;
+        if (from != g.me && nnz == 1) {
+          const Face full = region_face(f, rfull);
+          if (full.contiguous) { m.face = full; m.zero_copy = true; }
+        }
         if (!m.zero_copy) { m.off = recv_bytes; recv_bytes += round_up(m.face.bytes, MSG_ALIGN); }
         any_remote |= from != g.me;
         recvs.push_back(m);
       }
       if (to != PROC_NULL) {
         Msg m{i, key, to, region_face(f, sr), 0, false};
-        m.zero_copy = m.face.contiguous && to != g.me;
+        if (to != g.me) {
+          if (nnz == 1) {
+            const Face full = region_face(f, sfull);
+            if (full.contiguous) { m.face = full; m.zero_copy = true; }
+          } else {
+            m.zero_copy = m.face.contiguous;  // sends only read: safe
+          }
+        }
         if (!m.zero_copy) { m.off = send_bytes; send_bytes += round_up(m.face.bytes, MSG_ALIGN); }
         sends.push_back(m);
       }

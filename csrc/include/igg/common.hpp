@@ -42,7 +42,9 @@ inline int64_t round_up(int64_t v, int64_t g) { return ((v + g - 1) / g) * g; }
 #define IGG_HIP_CHECK(expr)                                                    \
   do {                                                                         \
     hipError_t _e = (expr);                                                    \
-    if (_e != hipSuccess)                                                      \
+    if (_e != hipSuccess) {                                                    \
+      (void)hipGetLastError(); /* clear the sticky copy of this error */       \
       ::igg::fail("HIP error '", hipGetErrorString(_e), "' at ", __FILE__, ":", \
                   __LINE__, " in ", #expr);                                    \
+    }                                                                          \
   } while (0)

@@ -36,7 +36,11 @@ struct CopyBatch {
 };
 
 // Device: enqueue all copies (any count, split in MAX_BATCH chunks) on `stream`.
-void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream);
+// system_fence: every thread ends with a system-scope release fence, so stores
+// into a peer GPU's memory are performed before a following stream write
+// signals them (put transport).
+void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
+                   bool system_fence = false);
 
 // Host: perform all copies now (threaded above THREADCOPY_THRESHOLD bytes).
 void host_copy2d(const std::vector<Copy2D>& copies, int elem_bytes);

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "igg/comm.hpp"
+#include "igg/peer.hpp"
 #include "igg/copy.hpp"
 #include "igg/topology.hpp"
 
@@ -150,6 +151,10 @@ class HaloEngine {
   void exchange_dim_impl(const std::vector<Field>& fields, int dim, bool device,
                          hipStream_t stream);
   void exchange_onephase(const std::vector<Field>& fields, bool device, hipStream_t stream);
+  void exchange_put(const std::vector<Field>& fields, hipStream_t stream, PeerMesh& mesh);
+  // Receive / send regions of the one-phase message with receiver-side
+  // direction `key`; false if the field has no such message.
+  bool dir_regions(const Field& f, int key, Region& rr, Region& sr) const;
   bool active(const Field& f, int d) const;
   GridInfo grid_;
   HaloMode mode_ = HaloMode::Auto;

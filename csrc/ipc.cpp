@@ -1,0 +1,62 @@
+#include "igg/ipc.hpp"
+
+#include <cstring>
+
+namespace igg {
+
+void* ipc_malloc(size_t bytes, MemKind kind) {
+  void* p = nullptr;
+  switch (kind) {
+    case MemKind::Default: IGG_HIP_CHECK(hipMalloc(&p, bytes)); break;
+    case MemKind::FineGrained: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained)); break;
+    case MemKind::Signal: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipMallocSignalMemory)); break;
+    case MemKind::Uncached: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached)); break;
+    default: fail("ipc_malloc: unknown memory kind ", static_cast<int>(kind));
+  }
+  IGG_HIP_CHECK(hipMemset(p, 0, bytes));
+  IGG_HIP_CHECK(hipDeviceSynchronize());
+  return p;
+}
+
+void ipc_free(void* p) {
+  if (!p) return;
+  (void)hipDeviceSynchronize();
+  IGG_HIP_CHECK(hipFree(p));
+}
+
+std::string ipc_get_handle(void* p) {
+  hipIpcMemHandle_t h;
+  IGG_HIP_CHECK(hipIpcGetMemHandle(&h, p));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void* ipc_open(const std::string& handle) {
+  if (handle.size() != sizeof(hipIpcMemHandle_t))
+    fail("ipc_open: handle has ", handle.size(), " bytes, expected ", sizeof(hipIpcMemHandle_t));
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.data(), sizeof(h));
+  void* p = nullptr;
+  IGG_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  return p;
+}
+
+void ipc_close(void* p) {
+  if (p) IGG_HIP_CHECK(hipIpcCloseMemHandle(p));
+}
+
+void stream_write_u64(hipStream_t s, void* p, uint64_t v) {
+  IGG_HIP_CHECK(hipStreamWriteValue64(s, p, v, 0));
+}
+
+void stream_wait_u64_geq(hipStream_t s, void* p, uint64_t v) {
+  IGG_HIP_CHECK(hipStreamWaitValue64(s, p, v, hipStreamWaitValueGte, ~uint64_t(0)));
+}
+
+bool can_stream_wait_value() {
+  int dev = 0, v = 0;
+  IGG_HIP_CHECK(hipGetDevice(&dev));
+  IGG_HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, dev));
+  return v != 0;
+}
+
+}  // namespace igg

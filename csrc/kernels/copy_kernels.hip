@@ -20,7 +20,7 @@ constexpr int64_t CHUNK = BLOCK * EPT;         // elements of a row per workgrou
 
 struct alignas(16) B16 { uint64_t x, y; };
 
-template <typename T>
+template <typename T, bool FENCE>
 __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch batch) {
   const int64_t b = blockIdx.x;
   int c = 0;
@@ -45,24 +45,27 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
     const int64_t i = i0 + k * BLOCK + threadIdx.x;
     if (i < n) dst[i * cp.dst_si] = v[k];
   }
+  if (FENCE) __threadfence_system();
 }
 
 // Copies whose rows are short (n_inner < 64, e.g. a face whose inner extent is
 // tiny or an edge/corner message) are flattened: one element per lane.
-template <typename T>
+template <typename T, bool FENCE>
 __global__ void __launch_bounds__(BLOCK) copy2d_flat_kernel(const CopyBatch batch) {
   const int64_t b = blockIdx.x;
   int c = 0;
   while (c + 1 < batch.n && b >= batch.block_start[c + 1]) ++c;
   const Copy2D& cp = batch.c[c];
   const int64_t e = (b - batch.block_start[c]) * BLOCK + threadIdx.x;
-  if (e >= cp.n_outer * cp.n_inner) return;
-  const int64_t o = e / cp.n_inner, i = e - o * cp.n_inner;
-  reinterpret_cast<T*>(cp.dst)[o * cp.dst_so + i * cp.dst_si] =
-      reinterpret_cast<const T*>(cp.src)[o * cp.src_so + i * cp.src_si];
+  if (e < cp.n_outer * cp.n_inner) {
+    const int64_t o = e / cp.n_inner, i = e - o * cp.n_inner;
+    reinterpret_cast<T*>(cp.dst)[o * cp.dst_so + i * cp.dst_si] =
+        reinterpret_cast<const T*>(cp.src)[o * cp.src_so + i * cp.src_si];
+  }
+  if (FENCE) __threadfence_system();
 }
 
-template <typename T>
+template <typename T, bool FENCE>
 void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream) {
   for (int flat = 0; flat < 2; ++flat) {
     size_t pos = 0;
@@ -86,10 +89,10 @@ void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream) {
       batch.block_start[batch.n] = blocks;
       if (blocks > 0x7fffffffLL) fail("launch_copy2d: too many blocks (", blocks, ")");
       if (flat)
-        hipLaunchKernelGGL(copy2d_flat_kernel<T>, dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
+        hipLaunchKernelGGL((copy2d_flat_kernel<T, FENCE>), dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
                            stream, batch);
       else
-        hipLaunchKernelGGL(copy2d_batch_kernel<T>, dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
+        hipLaunchKernelGGL((copy2d_batch_kernel<T, FENCE>), dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
                            stream, batch);
       IGG_HIP_CHECK(hipGetLastError());
     }
@@ -98,16 +101,23 @@ void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream) {
 
 }  // namespace
 
-void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream) {
-  if (copies.empty()) return;
+template <bool FENCE>
+void launch_sized(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream) {
   switch (elem_bytes) {
-    case 1: launch_typed<uint8_t>(copies, stream); break;
-    case 2: launch_typed<uint16_t>(copies, stream); break;
-    case 4: launch_typed<uint32_t>(copies, stream); break;
-    case 8: launch_typed<uint64_t>(copies, stream); break;
-    case 16: launch_typed<B16>(copies, stream); break;
+    case 1: launch_typed<uint8_t, FENCE>(copies, stream); break;
+    case 2: launch_typed<uint16_t, FENCE>(copies, stream); break;
+    case 4: launch_typed<uint32_t, FENCE>(copies, stream); break;
+    case 8: launch_typed<uint64_t, FENCE>(copies, stream); break;
+    case 16: launch_typed<B16, FENCE>(copies, stream); break;
     default: fail("launch_copy2d: unsupported element size ", elem_bytes, " bytes");
   }
+}
+
+void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
+                   bool system_fence) {
+  if (copies.empty()) return;
+  if (system_fence) launch_sized<true>(copies, elem_bytes, stream);
+  else launch_sized<false>(copies, elem_bytes, stream);
 }
 
 }  // namespace igg

@@ -1,0 +1,91 @@
+#include "igg/peer.hpp"
+
+#include "igg/ipc.hpp"
+
+namespace igg {
+
+PeerMesh::PeerMesh(int rank, int nranks, AllGather allgather)
+    : rank_(rank), nranks_(nranks), allgather_(std::move(allgather)) {
+  if (nranks < 1 || rank < 0 || rank >= nranks) fail("PeerMesh: invalid rank ", rank, " of ", nranks);
+  peer_flags_.assign(nranks, nullptr);
+  peer_arena_.assign(nranks, nullptr);
+  flags_ = static_cast<uint64_t*>(ipc_malloc(NFLAGS * sizeof(uint64_t), MemKind::Uncached));
+  exchange_handles(true);
+}
+
+PeerMesh::~PeerMesh() {
+  // Non-collective fallback: unmap peers, free own memory (the collective
+  // close() should have run first; by then these are no-ops).
+  for (int r = 0; r < nranks_; ++r) {
+    if (r == rank_) continue;
+    if (peer_arena_[r]) (void)hipIpcCloseMemHandle(peer_arena_[r]);
+    if (peer_flags_[r]) (void)hipIpcCloseMemHandle(peer_flags_[r]);
+    peer_arena_[r] = nullptr;
+    peer_flags_[r] = nullptr;
+  }
+  if (arena_) (void)hipFree(arena_);
+  if (flags_) (void)hipFree(flags_);
+  arena_ = nullptr;
+  flags_ = nullptr;
+}
+
+void PeerMesh::exchange_handles(bool flags_too) {
+  std::string mine;
+  if (flags_too) mine += ipc_get_handle(flags_);
+  if (arena_) mine += ipc_get_handle(arena_);
+  const std::vector<std::string> all = allgather_(mine);
+  if (static_cast<int>(all.size()) != nranks_) fail("PeerMesh: allgather returned ", all.size(), " entries");
+  const size_t hb = sizeof(hipIpcMemHandle_t);
+  for (int r = 0; r < nranks_; ++r) {
+    if (r == rank_) continue;
+    const std::string& h = all[r];
+    size_t pos = 0;
+    if (flags_too) {
+      peer_flags_[r] = static_cast<uint64_t*>(ipc_open(h.substr(pos, hb)));
+      pos += hb;
+    }
+    if (arena_) peer_arena_[r] = static_cast<char*>(ipc_open(h.substr(pos, hb)));
+  }
+}
+
+void PeerMesh::ensure_arena(size_t bytes) {
+  if (closed_) fail("PeerMesh: used after close()");
+  if (bytes <= arena_bytes_) return;
+  bytes = static_cast<size_t>(round_up(static_cast<int64_t>(bytes), 1 << 20));
+  // Every rank drains its own puts/unpacks into the old arenas, then agrees
+  // (allgather = barrier) before anyone unmaps or frees them.
+  IGG_HIP_CHECK(hipDeviceSynchronize());
+  (void)allgather_(std::string());
+  for (int r = 0; r < nranks_; ++r)
+    if (r != rank_ && peer_arena_[r]) {
+      ipc_close(peer_arena_[r]);
+      peer_arena_[r] = nullptr;
+    }
+  (void)allgather_(std::string());
+  if (arena_) ipc_free(arena_);
+  arena_ = static_cast<char*>(ipc_malloc(bytes, MemKind::Uncached));
+  arena_bytes_ = bytes;
+  exchange_handles(false);
+}
+
+void PeerMesh::close() {
+  if (closed_) return;
+  IGG_HIP_CHECK(hipDeviceSynchronize());
+  (void)allgather_(std::string());
+  for (int r = 0; r < nranks_; ++r) {
+    if (r == rank_) continue;
+    if (peer_arena_[r]) ipc_close(peer_arena_[r]);
+    if (peer_flags_[r]) ipc_close(peer_flags_[r]);
+    peer_arena_[r] = nullptr;
+    peer_flags_[r] = nullptr;
+  }
+  (void)allgather_(std::string());
+  if (arena_) ipc_free(arena_);
+  if (flags_) ipc_free(flags_);
+  arena_ = nullptr;
+  flags_ = nullptr;
+  arena_bytes_ = 0;
+  closed_ = true;
+}
+
+}  // namespace igg

@@ -14,7 +14,11 @@ MPI is not part of the MI355X stack; the replacement is
   streams by the C++ halo engine, no Python on the data path.
 
 ``IGG_TRANSPORT=torch`` swaps the native RCCL transport for torch.distributed's
-``nccl`` (= RCCL) ``batch_isend_irecv`` (debug/A-B only).
+``nccl`` (= RCCL) ``batch_isend_irecv`` (debug/A-B only); ``staged`` stages
+device halos through host memory over gloo (the reference's non-GPU-aware MPI
+path); ``put`` is the one-sided intra-node transport of csrc/peer.cpp (pack
+kernels store straight into IPC-mapped peer arenas, CP flag signalling) that
+lets the halo exchange run next to a stencil occupying the GPU.
 """
 from __future__ import annotations
 
@@ -96,6 +100,7 @@ class Communicator:
     size: int = 1
     rccl: object = None
     torch_nccl: object = None
+    mesh: object = None  # native.PeerMesh of the 'put' transport
     local_rank: int = 0
     local_size: int = 1
     _transports: dict = field(default_factory=dict)
@@ -147,6 +152,13 @@ class Communicator:
                 t = native.PyTransport(self._staged_p2p, False, True, "gloo-staged")
                 self._transports["staged"] = t
             return t
+        if choice == "put":
+            t = self._transports.get("put")
+            if t is None:
+                self.mesh = native.PeerMesh(self.rank, self.size, self._allgather_bytes)
+                t = native.PutTransport(self.mesh)
+                self._transports["put"] = t
+            return t
         if choice == "torch":
             t = self._transports.get("torch")
             if t is None:
@@ -156,6 +168,9 @@ class Communicator:
             return t
         self.ensure_rccl()
         return self.rccl
+
+    def _allgather_bytes(self, b: bytes) -> list:
+        return self.all_gather_object(bytes(b))
 
     def ensure_rccl(self):
         if self.rccl is None and self.size > 1:
@@ -209,6 +224,12 @@ class Communicator:
                 r.wait()
 
     def destroy(self) -> None:
+        if self.mesh is not None:
+            try:
+                self.mesh.close()  # collective: unmap peers, free arenas/flags
+            except Exception:
+                pass
+            self.mesh = None
         if self.rccl is not None:
             try:
                 native.device_synchronize()

@@ -167,7 +167,8 @@ def enable_loopback(dims=(True, True, True)) -> None:
     Every selected dimension gets both neighbours = rank 0 while the engine
     believes it is rank 1, so each face takes the full remote path — pack ->
     grouped ncclSend/ncclRecv over a 1-rank RCCL communicator (to itself) ->
-    unpack — with real RCCL kernels competing for CUs, exactly like an
+    unpack (or, with IGG_TRANSPORT=put, put kernel -> own arena -> flags ->
+    unpack) — with real communication kernels competing for CUs, like an
     interior rank of a multi-GPU run. The grid's neighbour table is updated
     too, so apps enable their boundary/interior overlap. Results equal a
     periodic exchange.
@@ -179,7 +180,10 @@ def enable_loopback(dims=(True, True, True)) -> None:
     for d in range(NDIMS):
         if dims[d]:
             gg.neighbors[:, d] = 0
-    _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
+    if config.transport_choice() == "put":
+        _loopback_comm = native.PutTransport(native.PeerMesh(0, 1, lambda b: [bytes(b)]))
+    else:
+        _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
     nb = gg.neighbors.tolist()
     peers = [0 if all(dims[d] or c == 1 for d, c in enumerate((k // 9, (k // 3) % 3, k % 3))) else PROC_NULL
              for k in range(27)]

@@ -60,8 +60,8 @@ def parse_loopvectorization(env: Mapping[str, str] | None = None) -> list[bool]:
 def transport_choice(env: Mapping[str, str] | None = None) -> str:
     env = os.environ if env is None else env
     t = env.get("IGG_TRANSPORT", "rccl").strip().lower()
-    if t not in ("rccl", "torch", "staged"):
-        raise ValueError(f"IGG_TRANSPORT must be 'rccl', 'torch' or 'staged' (got {t!r})")
+    if t not in ("rccl", "torch", "staged", "put"):
+        raise ValueError(f"IGG_TRANSPORT must be 'rccl', 'torch', 'staged' or 'put' (got {t!r})")
     return t
 
 

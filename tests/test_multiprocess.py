@@ -70,3 +70,22 @@ def test_diffusion_gpu_multirank_staged_overlap():
 @pytest.mark.gpu
 def test_gather_gpu_multirank_staged():
     run_ranks(4, "gather", "gpu", "f64", env_extra=GPU_ENV)
+
+
+# --- the one-sided 'put' transport (IPC-mapped arenas + stream flag ops); on
+# the one-GPU box every rank maps the same device, which exercises the whole
+# protocol (layout agreement, epochs, parity reuse, arena growth) bitwise.
+PUT_ENV = {"IGG_TRANSPORT": "put"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,cfg", [(2, (7, 5, 6, 1, 1, 1)), (8, (7, 5, 6, 0, 0, 0)), (4, (9, 6, 5, 1, 0, 1)),
+                                        (3, (6, 5, 4, 1, 1, 0))])
+def test_halo_gpu_multirank_put(nprocs, cfg):
+    run_ranks(nprocs, "halo", "gpu", *cfg, "f64", env_extra=PUT_ENV)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_diffusion_gpu_multirank_put(overlap):
+    run_ranks(8, "diffusion", "gpu", 24, 20, 18, 7, overlap, env_extra=PUT_ENV)
