@@ -29,16 +29,25 @@ T = torch.rand((n, n, n), dtype=torch.float64, device="cuda")
 Cp = 1 + torch.rand((n, n, n), dtype=torch.float64, device="cuda")
 T2 = T.clone()
 res = {}
-for v in (11, 0):
+import argparse  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--variants", default="11,0")
+ap.add_argument("--zw", default="tile", help="z slab width: 'tile' (tile-1) or an integer")
+ap.add_argument("--rounds", default="0,-4")
+a = ap.parse_args()
+for v in [int(x) for x in a.variants.split(",")]:
     W = native.diffusion3d_variant_tile(v)
-    slabs, interior = stencil.split_boundary((n, n, n), [1, 1, 1], (1, 1, W - 1))
+    zw = W - 1 if a.zw == "tile" else int(a.zw)
+    slabs, interior = stencil.split_boundary((n, n, n), [1, 1, 1], (1, 1, zw))
     names = ["x_lo", "x_hi", "y_lo", "y_hi", "z_lo", "z_hi"]
-    for rounds in (0, -4):
+    for rounds in [int(x) for x in a.rounds.split(",")]:
         def run(boxes):
             return lambda: native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], [1.0] * 3, 0.01,
                                               8, boxes, True, v, torch.cuda.current_stream().cuda_stream, rounds)
         r = {nm: t(run([b])) for nm, b in zip(names, slabs)}
         r["all_slabs"] = t(run(slabs))
+        r["sum_separate"] = round(sum(r[nm] for nm in names), 4)
         r["interior"] = t(run([interior]))
         r["full"] = t(run([((1, 1, 1), (n - 1, n - 1, n - 1))]))
         res[f"v{v}_r{rounds}"] = r

@@ -284,13 +284,10 @@ PYBIND11_MODULE(_igg_native, m) {
       .def_property_readonly("rank", &PeerMesh::rank)
       .def_property_readonly("nranks", &PeerMesh::nranks)
       .def_property_readonly("arena_bytes", &PeerMesh::arena_bytes)
-      .def_property_readonly("epoch", &PeerMesh::epoch)
-      .def("flag", [](const PeerMesh& m, int idx) {
-        if (idx < 0 || idx >= PeerMesh::NFLAGS) fail("PeerMesh.flag: index out of range");
-        uint64_t v = 0;
-        IGG_HIP_CHECK(hipMemcpy(&v, m.flags(m.rank()) + idx, 8, hipMemcpyDeviceToHost));
-        return v;
-      })
+      .def_property_readonly("epoch", [](const PeerMesh& m) { return m.read_flag(PutFlags::EPOCH); })
+      .def_property_readonly("flag_words", &PeerMesh::flag_words)
+      .def("flag", &PeerMesh::read_flag)
+      .def("check_error", &PeerMesh::check_error)
       .def("close", &PeerMesh::close);
   py::class_<PutTransport, Transport, std::shared_ptr<PutTransport>>(m, "PutTransport")
       .def(py::init<std::shared_ptr<PeerMesh>>(), py::arg("mesh"))

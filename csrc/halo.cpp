@@ -209,9 +209,8 @@ void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) 
   }
   auto* put = device ? dynamic_cast<PutTransport*>(dev_transport_.get()) : nullptr;
   if (put) {
-    // Stream flag values are baked into a captured graph, but every exchange
-    // needs a new epoch: the put transport cannot be replayed from a graph.
-    if (capturing) fail("update_halo: the 'put' transport cannot be captured in a hipGraph.");
+    // Kernel arguments are epoch-independent (the epoch lives on the device),
+    // so a captured exchange replays correctly.
     exchange_put(fields, stream, put->mesh());
   } else if (resolved_mode(fields) == HaloMode::OnePhase) {
     exchange_onephase(fields, device, stream);
@@ -405,77 +404,65 @@ void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stre
     }
   }
   mesh.ensure_arena(2 * per);  // collective, grow-only
-  const uint64_t k = mesh.next_epoch();
-  // Fixed halves per parity (independent of this call's layout), so messages
-  // of exchange k-1 and k never share bytes whatever fields either carried.
-  const size_t pbase = (k & 1) * (mesh.arena_bytes() / 2);
+  // Fixed halves per epoch parity (independent of this call's layout); the
+  // kernels pick the half from the device-resident epoch.
+  const int64_t half = static_cast<int64_t>(mesh.arena_bytes() / 2);
   const int me = mesh.rank();
   std::vector<Copy2D> put, unpack;
-  std::vector<int> out_keys, in_keys;
+  std::vector<int> out_ranks, in_ranks, nb_ranks;
+  auto add = [](std::vector<int>& v, int r) {
+    if (std::find(v.begin(), v.end(), r) == v.end()) v.push_back(r);
+  };
   for (int key = 0; key < 27; ++key) {
     if (key == 13) continue;
     const int64_t from = g.peers[key], to = g.peers[26 - key];
-    bool any_in = false, any_out = false;
+    if (from != PROC_NULL) add(nb_ranks, static_cast<int>(from));
     for (size_t i = 0; i < nf; ++i) {
       const Field& f = fields[i];
       Region rr{}, sr{};
       if (!dir_regions(f, key, rr, sr)) continue;
-      const size_t off = pbase + slot[key * nf + i];
+      const size_t off = slot[key * nf + i];
       if (to != PROC_NULL) {
         const Face sf = region_face(f, sr);
         put.push_back({sf.base, mesh.arena(static_cast<int>(to)) + off, sf.n_outer, sf.n_inner, sf.s_outer,
                        sf.s_inner, sf.n_inner, 1});
-        any_out = true;
+        add(out_ranks, static_cast<int>(to));
       }
       if (from != PROC_NULL) {
         const Face rf = region_face(f, rr);
         unpack.push_back({mesh.arena(me) + off, rf.base, rf.n_outer, rf.n_inner, rf.n_inner, 1, rf.s_outer,
                           rf.s_inner});
-        any_in = true;
+        add(in_ranks, static_cast<int>(from));
       }
     }
-    if (any_out) out_keys.push_back(key);
-    if (any_in) in_keys.push_back(key);
   }
   last_msgs_ = static_cast<int>(put.size());
-  // 1. each receiver has finished unpacking exchange k-2 (the last one that
-  //    used this parity of its arena); slot = my direction towards it.
-  if (k > 2)
-    for (int key : out_keys) stream_wait_u64_geq(stream, mesh.flags(me) + PeerMesh::FREED + (26 - key), k - 2);
-  // 2. pack straight into the receivers' arenas (stores over xGMI), 3. signal
-  launch_copy2d(put, eb, stream, /*system_fence=*/true);
-  for (int key : out_keys)
-    stream_write_u64(stream, mesh.flags(static_cast<int>(g.peers[26 - key])) + PeerMesh::ARRIVED + key, k);
-  // 4. wait for my messages, unpack them, then tell EVERY neighbour that my
-  //    arena is consumed up to epoch k (also those that sent nothing now:
-  //    they may send next time, into a layout that overlaps this one).
-  for (int key : in_keys) stream_wait_u64_geq(stream, mesh.flags(me) + PeerMesh::ARRIVED + key, k);
-  launch_copy2d(unpack, eb, stream);
-  for (int key = 0; key < 27; ++key)
-    if (key != 13 && g.peers[key] != PROC_NULL)
-      stream_write_u64(stream, mesh.flags(static_cast<int>(g.peers[key])) + PeerMesh::FREED + (26 - key), k);
+  if (out_ranks.size() > PUT_MAX_PEERS || in_ranks.size() > PUT_MAX_PEERS || nb_ranks.size() > PUT_MAX_PEERS)
+    fail("put transport: too many distinct peers");
+  PutSync ps{};
+  ps.my_flags = mesh.flags(me);
+  ps.my_rank = me;
+  ps.nranks = mesh.nranks();
+  ps.timeout_ticks = mesh.timeout_ticks();
+  ps.n_out = static_cast<int>(out_ranks.size());
+  ps.n_in = static_cast<int>(in_ranks.size());
+  ps.n_nb = static_cast<int>(nb_ranks.size());
+  for (int j = 0; j < ps.n_out; ++j) {
+    ps.out_rank[j] = out_ranks[j];
+    ps.out_flags[j] = mesh.flags(out_ranks[j]);
+  }
+  for (int j = 0; j < ps.n_in; ++j) ps.in_rank[j] = in_ranks[j];
+  for (int j = 0; j < ps.n_nb; ++j) ps.nb_flags[j] = mesh.flags(nb_ranks[j]);
+  const uint64_t* epoch = mesh.flags(me) + PutFlags::EPOCH;
+  // begin -> put (stores into the receivers' arenas) -> sync -> unpack
+  launch_put_begin(ps, stream);
+  launch_copy2d(put, eb, stream, /*system_fence=*/true, ParityShift{epoch, half, 1});
+  launch_put_sync(ps, stream);
+  launch_copy2d(unpack, eb, stream, false, ParityShift{epoch, half, 2});
   static const bool debug = std::getenv("IGG_PUT_DEBUG") != nullptr;
   if (debug) {
-    // Bounded drain with a report of the flags this rank waits on.
-    std::fprintf(stderr, "[put rank %d] epoch %llu: %zu puts, %zu unpacks, out keys %zu, in keys %zu\n", me,
-                 static_cast<unsigned long long>(k), put.size(), unpack.size(), out_keys.size(), in_keys.size());
-    for (int it = 0; it < 5000 && hipStreamQuery(stream) == hipErrorNotReady; ++it) usleep(1000);
-    if (hipStreamQuery(stream) == hipErrorNotReady) {
-      hipStream_t side;
-      IGG_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-      uint64_t fl[PeerMesh::NFLAGS];
-      IGG_HIP_CHECK(hipMemcpyAsync(fl, mesh.flags(me), sizeof(fl), hipMemcpyDeviceToHost, side));
-      IGG_HIP_CHECK(hipStreamSynchronize(side));
-      for (int key : in_keys)
-        std::fprintf(stderr, "[put rank %d] STUCK epoch %llu: arrived[%d]=%llu from %lld\n", me,
-                     static_cast<unsigned long long>(k), key, static_cast<unsigned long long>(fl[key]),
-                     static_cast<long long>(g.peers[key]));
-      for (int key : out_keys)
-        std::fprintf(stderr, "[put rank %d]   freed[%d]=%llu (to %lld)\n", me, 26 - key,
-                     static_cast<unsigned long long>(fl[PeerMesh::FREED + 26 - key]),
-                     static_cast<long long>(g.peers[26 - key]));
-      fail("put transport: exchange did not complete within 5 s (IGG_PUT_DEBUG)");
-    }
+    IGG_HIP_CHECK(hipStreamSynchronize(stream));
+    mesh.check_error();
   }
 }
 

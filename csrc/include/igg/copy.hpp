@@ -27,20 +27,32 @@ struct Copy2D {
   int64_t dst_so, dst_si;
 };
 
-constexpr int MAX_BATCH = 24;  // keeps the kernel argument block < 4 KiB
+constexpr int MAX_BATCH = 32;  // all 26 one-phase directions in one launch; kernarg < 4 KiB
 
 struct CopyBatch {
   Copy2D c[MAX_BATCH];
   int64_t block_start[MAX_BATCH + 1];
   int n;
+  uint32_t flat_mask = 0;  // bit c: copy c has short rows -> one element per lane
+  // Put transport: a device-resident exchange epoch selects the arena half;
+  // parity_side 1 shifts every dst, 2 every src by parity_bytes when odd.
+  const uint64_t* epoch = nullptr;
+  int64_t parity_bytes = 0;
+  int parity_side = 0;
+};
+
+struct ParityShift {
+  const uint64_t* epoch = nullptr;
+  int64_t bytes = 0;
+  int side = 0;  // 0 none, 1 dst, 2 src
 };
 
 // Device: enqueue all copies (any count, split in MAX_BATCH chunks) on `stream`.
-// system_fence: every thread ends with a system-scope release fence, so stores
-// into a peer GPU's memory are performed before a following stream write
-// signals them (put transport).
+// system_fence: every thread ends by waiting for its stores to be acknowledged
+// (put transport: stores into a peer's uncached arena are performed before the
+// following sync kernel publishes them).
 void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
-                   bool system_fence = false);
+                   bool system_fence = false, const ParityShift& parity = ParityShift{});
 
 // Host: perform all copies now (threaded above THREADCOPY_THRESHOLD bytes).
 void host_copy2d(const std::vector<Copy2D>& copies, int elem_bytes);

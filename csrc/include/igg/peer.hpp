@@ -1,23 +1,18 @@
 // Put transport: one-sided halo exchange between the GPUs of a node through
 // IPC-mapped receive arenas, with command-processor flag signalling.
 //
-// Per exchange (epoch k, arena half p = k & 1), for every message S -> R with
-// receiver-side direction key u (dir_key order, halo.hpp; S = R + u):
-//   S: wait  S.freed[26-u] >= k-2   (R finished unpacking exchange k-2, the
-//                                     last one that used half p of its arena)
-//   S: put kernel: S's send region -> R.arena[p][slot(u, field)] (xGMI stores)
-//   S: write R.arrived[u] = k
-//   R: wait  R.arrived[u] >= k ; unpack kernel from R.arena[p]
-//   R: write N.freed[26-u'] = k for EVERY neighbour N = R + u' (also those
-//      that sent nothing this time: the next call may use another layout)
-// Slots depend only on field shapes, so sender and receiver agree without
-// negotiation; the two halves let exchange k+1's puts land while exchange k is
-// still being unpacked. Waits/writes are
-// hipStreamWaitValue64/WriteValue64 on the caller's stream; nothing blocks the
-// host and no workgroup spins on a flag while the stencil owns the CUs.
+// Protocol (device-driven, no host in the loop; kernels in put.hpp): per
+// exchange e every rank bumps its device epoch, signals "consumed e-1" to all
+// neighbours, waits until its receivers consumed e-2 (the last exchange that
+// used arena half e&1), packs straight into the receivers' arenas (stores over
+// xGMI), publishes arrived[me] = e at each receiver, waits for arrived[s] >= e
+// of each sender and unpacks from its own arena. Arena slots depend only on
+// field shapes, so sender and receiver agree without negotiation; the two
+// halves let exchange e+1's puts land while e is still being unpacked.
 //
 // Arenas and flags are uncached device memory (coherent across devices: remote
-// stores and CP writes land in HBM, local reads bypass L2), exported once with
+// stores land in HBM without passing through any L2, local reads bypass L2, so
+// the only release needed is "stores acknowledged"), exported once with
 // hipIpcGetMemHandle and re-exported (collectively) only when an arena grows.
 #pragma once
 
@@ -28,6 +23,8 @@
 #include <vector>
 
 #include "igg/comm.hpp"
+#include "igg/ipc.hpp"
+#include "igg/put.hpp"
 
 namespace igg {
 
@@ -35,8 +32,6 @@ class PeerMesh {
  public:
   // allgather(bytes) -> bytes of every rank (rank order); collective over the mesh.
   using AllGather = std::function<std::vector<std::string>(const std::string&)>;
-  static constexpr int NFLAGS = 64;  // [0,27): arrived[u], [32,59): freed[u]
-  static constexpr int ARRIVED = 0, FREED = 32;
 
   PeerMesh(int rank, int nranks, AllGather allgather);
   ~PeerMesh();
@@ -50,8 +45,12 @@ class PeerMesh {
   size_t arena_bytes() const { return arena_bytes_; }
   char* arena(int r) const { return r == rank_ ? arena_ : peer_arena_.at(r); }
   uint64_t* flags(int r) const { return r == rank_ ? flags_ : peer_flags_.at(r); }
-  uint64_t next_epoch() { return ++epoch_; }
-  uint64_t epoch() const { return epoch_; }
+  int flag_words() const { return PutFlags::words(nranks_); }
+  // Host read of one of my flag words (side stream; never blocks on halo work).
+  uint64_t read_flag(int idx) const;
+  // Raises igg::Error if a put-transport kernel timed out waiting for a peer.
+  void check_error() const;
+  int64_t timeout_ticks() const { return timeout_ticks_; }
   // Collective teardown (also run by the destructor without the collectives).
   void close();
 
@@ -64,7 +63,9 @@ class PeerMesh {
   size_t arena_bytes_ = 0;
   std::vector<uint64_t*> peer_flags_;
   std::vector<char*> peer_arena_;
-  uint64_t epoch_ = 0;
+  int64_t timeout_ticks_ = 0;
+  MemKind arena_kind_ = MemKind::Uncached;
+  hipStream_t side_ = nullptr;
   bool closed_ = false;
 };
 

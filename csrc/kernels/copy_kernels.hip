@@ -20,6 +20,15 @@ constexpr int64_t CHUNK = BLOCK * EPT;         // elements of a row per workgrou
 
 struct alignas(16) B16 { uint64_t x, y; };
 
+// Byte shift of the arena half selected by the device-resident epoch (odd ->
+// second half). The epoch lives in uncached memory written by the put
+// transport's begin kernel earlier on the same stream.
+__device__ __forceinline__ int64_t parity_shift(const CopyBatch& b) {
+  if (b.parity_side == 0) return 0;
+  const uint64_t e = __hip_atomic_load(b.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return (e & 1) ? b.parity_bytes : 0;
+}
+
 template <typename T, bool FENCE>
 __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch batch) {
   const int64_t b = blockIdx.x;
@@ -28,96 +37,93 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
   while (c + 1 < batch.n && b >= batch.block_start[c + 1]) ++c;
   const Copy2D& cp = batch.c[c];
   const int64_t local = b - batch.block_start[c];
-  const int64_t nchunks = (cp.n_inner + CHUNK - 1) / CHUNK;
-  const int64_t o = local / nchunks;              // row (outer index)
-  const int64_t i0 = (local - o * nchunks) * CHUNK;
-  const T* __restrict__ src = reinterpret_cast<const T*>(cp.src) + o * cp.src_so;
-  T* __restrict__ dst = reinterpret_cast<T*>(cp.dst) + o * cp.dst_so;
-  const int64_t n = cp.n_inner;
-  T v[EPT];
-#pragma unroll
-  for (int k = 0; k < EPT; ++k) {
-    const int64_t i = i0 + k * BLOCK + threadIdx.x;
-    if (i < n) v[k] = src[i * cp.src_si];
-  }
-#pragma unroll
-  for (int k = 0; k < EPT; ++k) {
-    const int64_t i = i0 + k * BLOCK + threadIdx.x;
-    if (i < n) dst[i * cp.dst_si] = v[k];
-  }
-  if (FENCE) __threadfence_system();
-}
-
-// Copies whose rows are short (n_inner < 64, e.g. a face whose inner extent is
-// tiny or an edge/corner message) are flattened: one element per lane.
-template <typename T, bool FENCE>
-__global__ void __launch_bounds__(BLOCK) copy2d_flat_kernel(const CopyBatch batch) {
-  const int64_t b = blockIdx.x;
-  int c = 0;
-  while (c + 1 < batch.n && b >= batch.block_start[c + 1]) ++c;
-  const Copy2D& cp = batch.c[c];
-  const int64_t e = (b - batch.block_start[c]) * BLOCK + threadIdx.x;
-  if (e < cp.n_outer * cp.n_inner) {
-    const int64_t o = e / cp.n_inner, i = e - o * cp.n_inner;
-    reinterpret_cast<T*>(cp.dst)[o * cp.dst_so + i * cp.dst_si] =
-        reinterpret_cast<const T*>(cp.src)[o * cp.src_so + i * cp.src_si];
-  }
-  if (FENCE) __threadfence_system();
-}
-
-template <typename T, bool FENCE>
-void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream) {
-  for (int flat = 0; flat < 2; ++flat) {
-    size_t pos = 0;
-    while (pos < copies.size()) {
-      CopyBatch batch{};
-      batch.n = 0;
-      int64_t blocks = 0;
-      while (pos < copies.size() && batch.n < MAX_BATCH) {
-        const Copy2D& c = copies[pos++];
-        const int64_t total = c.n_outer * c.n_inner;
-        if (total <= 0) continue;
-        const bool is_flat = c.n_inner < 64;
-        if (is_flat != (flat == 1)) continue;
-        batch.c[batch.n] = c;
-        batch.block_start[batch.n] = blocks;
-        blocks += is_flat ? (total + BLOCK - 1) / BLOCK
-                          : c.n_outer * ((c.n_inner + CHUNK - 1) / CHUNK);
-        ++batch.n;
-      }
-      if (batch.n == 0) continue;
-      batch.block_start[batch.n] = blocks;
-      if (blocks > 0x7fffffffLL) fail("launch_copy2d: too many blocks (", blocks, ")");
-      if (flat)
-        hipLaunchKernelGGL((copy2d_flat_kernel<T, FENCE>), dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
-                           stream, batch);
-      else
-        hipLaunchKernelGGL((copy2d_batch_kernel<T, FENCE>), dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
-                           stream, batch);
-      IGG_HIP_CHECK(hipGetLastError());
+  const int64_t shift = parity_shift(batch);
+  const char* sbase = cp.src + (batch.parity_side == 2 ? shift : 0);
+  char* dbase = cp.dst + (batch.parity_side == 1 ? shift : 0);
+  if ((batch.flat_mask >> c) & 1u) {
+    // Short rows (n_inner < 64: narrow faces, edges, corners): one element per
+    // lane over the flattened region.
+    const int64_t e = local * BLOCK + threadIdx.x;
+    if (e < cp.n_outer * cp.n_inner) {
+      const int64_t o = e / cp.n_inner, i = e - o * cp.n_inner;
+      reinterpret_cast<T*>(dbase)[o * cp.dst_so + i * cp.dst_si] =
+          reinterpret_cast<const T*>(sbase)[o * cp.src_so + i * cp.src_si];
     }
+  } else {
+    const int64_t nchunks = (cp.n_inner + CHUNK - 1) / CHUNK;
+    const int64_t o = local / nchunks;              // row (outer index)
+    const int64_t i0 = (local - o * nchunks) * CHUNK;
+    const T* __restrict__ src = reinterpret_cast<const T*>(sbase) + o * cp.src_so;
+    T* __restrict__ dst = reinterpret_cast<T*>(dbase) + o * cp.dst_so;
+    const int64_t n = cp.n_inner;
+    T v[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int64_t i = i0 + k * BLOCK + threadIdx.x;
+      if (i < n) v[k] = src[i * cp.src_si];
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int64_t i = i0 + k * BLOCK + threadIdx.x;
+      if (i < n) dst[i * cp.dst_si] = v[k];
+    }
+  }
+  // Put transport: the destination arena is uncached (stores bypass L2), so
+  // waiting for this thread's stores to be acknowledged is all the release
+  // needed before the sync kernel publishes the arrival flag.
+  if (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+}
+
+template <typename T, bool FENCE>
+void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream, const ParityShift& par) {
+  size_t pos = 0;
+  while (pos < copies.size()) {
+    CopyBatch batch{};
+    batch.n = 0;
+    batch.epoch = par.epoch;
+    batch.parity_bytes = par.bytes;
+    batch.parity_side = par.side;
+    int64_t blocks = 0;
+    while (pos < copies.size() && batch.n < MAX_BATCH) {
+      const Copy2D& c = copies[pos++];
+      const int64_t total = c.n_outer * c.n_inner;
+      if (total <= 0) continue;
+      const bool is_flat = c.n_inner < 64;
+      batch.c[batch.n] = c;
+      batch.block_start[batch.n] = blocks;
+      if (is_flat) batch.flat_mask |= 1u << batch.n;
+      blocks += is_flat ? (total + BLOCK - 1) / BLOCK : c.n_outer * ((c.n_inner + CHUNK - 1) / CHUNK);
+      ++batch.n;
+    }
+    if (batch.n == 0) continue;
+    batch.block_start[batch.n] = blocks;
+    if (blocks > 0x7fffffffLL) fail("launch_copy2d: too many blocks (", blocks, ")");
+    hipLaunchKernelGGL((copy2d_batch_kernel<T, FENCE>), dim3(static_cast<unsigned>(blocks)), dim3(BLOCK), 0,
+                       stream, batch);
+    IGG_HIP_CHECK(hipGetLastError());
   }
 }
 
 }  // namespace
 
 template <bool FENCE>
-void launch_sized(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream) {
+void launch_sized(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
+                  const ParityShift& par) {
   switch (elem_bytes) {
-    case 1: launch_typed<uint8_t, FENCE>(copies, stream); break;
-    case 2: launch_typed<uint16_t, FENCE>(copies, stream); break;
-    case 4: launch_typed<uint32_t, FENCE>(copies, stream); break;
-    case 8: launch_typed<uint64_t, FENCE>(copies, stream); break;
-    case 16: launch_typed<B16, FENCE>(copies, stream); break;
+    case 1: launch_typed<uint8_t, FENCE>(copies, stream, par); break;
+    case 2: launch_typed<uint16_t, FENCE>(copies, stream, par); break;
+    case 4: launch_typed<uint32_t, FENCE>(copies, stream, par); break;
+    case 8: launch_typed<uint64_t, FENCE>(copies, stream, par); break;
+    case 16: launch_typed<B16, FENCE>(copies, stream, par); break;
     default: fail("launch_copy2d: unsupported element size ", elem_bytes, " bytes");
   }
 }
 
 void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
-                   bool system_fence) {
+                   bool system_fence, const ParityShift& parity) {
   if (copies.empty()) return;
-  if (system_fence) launch_sized<true>(copies, elem_bytes, stream);
-  else launch_sized<false>(copies, elem_bytes, stream);
+  if (system_fence) launch_sized<true>(copies, elem_bytes, stream, parity);
+  else launch_sized<false>(copies, elem_bytes, stream, parity);
 }
 
 }  // namespace igg

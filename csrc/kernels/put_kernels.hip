@@ -1,0 +1,80 @@
+// Put-transport synchronisation kernels (one workgroup of one wave each).
+#include <hip/hip_runtime.h>
+
+#include "igg/common.hpp"
+#include "igg/put.hpp"
+
+namespace igg {
+namespace {
+
+__device__ __forceinline__ uint64_t load_sys(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void store_sys(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Spin until *p >= v; false (and an error code recorded) on timeout.
+__device__ bool wait_geq(const uint64_t* p, uint64_t v, const PutSync& s, uint64_t code) {
+  const long long t0 = wall_clock64();
+  while (load_sys(p) < v) {
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > s.timeout_ticks) {
+      uint64_t expected = 0;
+      __hip_atomic_compare_exchange_strong(s.my_flags + PutFlags::ERROR, &expected, code, __ATOMIC_RELAXED,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(64) put_begin_kernel(const PutSync s) {
+  __shared__ uint64_t epoch;
+  const int lane = threadIdx.x;
+  if (lane == 0) {
+    const uint64_t e = load_sys(s.my_flags + PutFlags::EPOCH) + 1;
+    store_sys(s.my_flags + PutFlags::EPOCH, e);
+    epoch = e;
+  }
+  __syncthreads();
+  const uint64_t e = epoch;
+  const int freed = PutFlags::freed(s.nranks);
+  // My unpack of e-1 completed before this kernel started (same stream).
+  if (lane < s.n_nb && e > 1) store_sys(s.nb_flags[lane] + freed + s.my_rank, e - 1);
+  if (lane < s.n_out && e > 2) wait_geq(s.my_flags + freed + s.out_rank[lane], e - 2, s, 0x100 + lane);
+}
+
+__global__ void __launch_bounds__(64) put_sync_kernel(const PutSync s) {
+  const int lane = threadIdx.x;
+  const uint64_t e = load_sys(s.my_flags + PutFlags::EPOCH);
+  // The put kernel(s) finished (stream order) with their stores acknowledged;
+  // one system-scope release here orders them before the flag stores.
+  __threadfence_system();
+  if (lane < s.n_out) store_sys(s.out_flags[lane] + PutFlags::ARRIVED + s.my_rank, e);
+  if (lane < s.n_in) wait_geq(s.my_flags + PutFlags::ARRIVED + s.in_rank[lane], e, s, 0x200 + lane);
+}
+
+}  // namespace
+
+void launch_put_begin(const PutSync& s, hipStream_t stream) {
+  if (s.n_out > 64 || s.n_nb > 64) fail("launch_put_begin: too many peers");
+  hipLaunchKernelGGL(put_begin_kernel, dim3(1), dim3(64), 0, stream, s);
+  IGG_HIP_CHECK(hipGetLastError());
+}
+
+void launch_put_sync(const PutSync& s, hipStream_t stream) {
+  if (s.n_out > 64 || s.n_in > 64) fail("launch_put_sync: too many peers");
+  hipLaunchKernelGGL(put_sync_kernel, dim3(1), dim3(64), 0, stream, s);
+  IGG_HIP_CHECK(hipGetLastError());
+}
+
+int64_t put_timeout_ticks(double seconds) {
+  int dev = 0, khz = 0;
+  IGG_HIP_CHECK(hipGetDevice(&dev));
+  IGG_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) khz = 100000;
+  return static_cast<int64_t>(seconds * khz * 1000.0);
+}
+
+}  // namespace igg

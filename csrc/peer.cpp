@@ -2,6 +2,9 @@
 
 #include "igg/ipc.hpp"
 
+#include <cstdlib>
+#include <ios>
+
 namespace igg {
 
 PeerMesh::PeerMesh(int rank, int nranks, AllGather allgather)
@@ -9,8 +12,30 @@ PeerMesh::PeerMesh(int rank, int nranks, AllGather allgather)
   if (nranks < 1 || rank < 0 || rank >= nranks) fail("PeerMesh: invalid rank ", rank, " of ", nranks);
   peer_flags_.assign(nranks, nullptr);
   peer_arena_.assign(nranks, nullptr);
-  flags_ = static_cast<uint64_t*>(ipc_malloc(NFLAGS * sizeof(uint64_t), MemKind::Uncached));
+  flags_ = static_cast<uint64_t*>(ipc_malloc(PutFlags::words(nranks) * sizeof(uint64_t), MemKind::Uncached));
+  IGG_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  double seconds = 120.0;
+  if (const char* t = std::getenv("IGG_PUT_TIMEOUT")) seconds = std::atof(t);
+  timeout_ticks_ = put_timeout_ticks(seconds);
+  if (const char* k = std::getenv("IGG_PUT_ARENA_KIND")) arena_kind_ = static_cast<MemKind>(std::atoi(k));
   exchange_handles(true);
+}
+
+uint64_t PeerMesh::read_flag(int idx) const {
+  if (idx < 0 || idx >= flag_words() || !flags_) fail("PeerMesh.read_flag: index ", idx, " out of range");
+  uint64_t v = 0;
+  IGG_HIP_CHECK(hipMemcpyAsync(&v, flags_ + idx, 8, hipMemcpyDeviceToHost, side_));
+  IGG_HIP_CHECK(hipStreamSynchronize(side_));
+  return v;
+}
+
+void PeerMesh::check_error() const {
+  if (!flags_) return;
+  const uint64_t e = read_flag(PutFlags::ERROR);
+  if (e != 0)
+    fail("put transport: a synchronisation kernel timed out waiting for a peer (code 0x", std::hex, e,
+         std::dec, "); the halo data of that exchange is invalid. Raise IGG_PUT_TIMEOUT if peers are "
+         "legitimately slow.");
 }
 
 PeerMesh::~PeerMesh() {
@@ -25,8 +50,10 @@ PeerMesh::~PeerMesh() {
   }
   if (arena_) (void)hipFree(arena_);
   if (flags_) (void)hipFree(flags_);
+  if (side_) (void)hipStreamDestroy(side_);
   arena_ = nullptr;
   flags_ = nullptr;
+  side_ = nullptr;
 }
 
 void PeerMesh::exchange_handles(bool flags_too) {
@@ -63,7 +90,7 @@ void PeerMesh::ensure_arena(size_t bytes) {
     }
   (void)allgather_(std::string());
   if (arena_) ipc_free(arena_);
-  arena_ = static_cast<char*>(ipc_malloc(bytes, MemKind::Uncached));
+  arena_ = static_cast<char*>(ipc_malloc(bytes, arena_kind_));
   arena_bytes_ = bytes;
   exchange_handles(false);
 }

@@ -136,11 +136,6 @@ class Diffusion3D:
         """
         if self.device.type != "cuda":
             raise RuntimeError("Diffusion3D.capture: hipGraphs need a GPU model")
-        from ..parallel import halo as _halo
-
-        if _halo.engine().transport_name(True) == "put":
-            raise RuntimeError("Diffusion3D.capture: the 'put' transport cannot be captured in a hipGraph "
-                               "(its flag epochs change every exchange)")
         if not self._warm:
             self.step()
         torch.cuda.synchronize()

@@ -262,6 +262,7 @@ def finalize_global_grid(*, finalize_MPI: bool = True) -> None:
     from . import gather as _gather
     from . import halo as _halo
 
+    _halo.check_transport()
     _gather.free_gather_buffer()
     _halo.free_update_halo_buffers()
     gg = _global_grid

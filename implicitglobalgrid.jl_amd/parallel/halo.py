@@ -147,6 +147,19 @@ def _drop_engine() -> None:
     _loopback_comm = None
 
 
+def check_transport() -> None:
+    """Raise if a put-transport synchronisation kernel timed out (its spin
+    waits are bounded; a timeout means some exchange's halo is invalid)."""
+    meshes = []
+    gg = _grid.global_grid()
+    if gg.comm is not None and getattr(gg.comm, "mesh", None) is not None:
+        meshes.append(gg.comm.mesh)
+    if _loopback_comm is not None and hasattr(_loopback_comm, "mesh"):
+        meshes.append(_loopback_comm.mesh)
+    for m in meshes:
+        m.check_error()
+
+
 def engine():
     _grid.check_initialized()
     return _engine

@@ -1,3 +1,7 @@
-mkdir -p gpurun_out/put
-timeout -k 10 500 python -m pytest tests/test_multiprocess.py tests/test_gpu_halo.py -x -v -k "put" > gpurun_out/put/mp.log 2>&1 || { tail -60 gpurun_out/put/mp.log; exit 1; }
-tail -10 gpurun_out/put/mp.log
+R=$PWD
+mkdir -p $R/gpurun_out/tr
+cd /tmp && export TMPDIR=/tmp
+for cu in 0 32; do
+IGG_TRANSPORT=put timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/tr/cu$cu -o run -- python3 $R/benchmarks/trace_step.py --ir 0 --hv 11 --hr 0 --cu $cu > $R/gpurun_out/tr/cu$cu.log 2>&1
+echo cu$cu rc=$?
+done

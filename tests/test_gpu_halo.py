@@ -223,8 +223,9 @@ def test_gpu_graph_replay_matches_eager(gpu, mode):
 
 def test_gpu_loopback_put_transport(gpu, monkeypatch):
     """Loopback through the put transport: every message is a put into the own
-    IPC-exportable arena + stream flag signalling; periodic oracle, bitwise,
-    over several exchanges (both arena parities, epoch-2 slot reuse)."""
+    IPC-exportable arena + device-side flag signalling; periodic oracle,
+    bitwise, over several exchanges (both arena halves, epoch-2 reuse), eager,
+    overlapped and replayed from a hipGraph."""
     from igg.models.diffusion3d import Diffusion3D
     from igg.parallel import halo as H
 
@@ -244,10 +245,16 @@ def test_gpu_loopback_put_transport(gpu, monkeypatch):
     # the model (eager, serial and overlapped) matches the RCCL-free periodic run
     m1 = Diffusion3D(dtype=torch.float64)
     m2 = Diffusion3D(dtype=torch.float64, overlap=True)
-    m1.run(6)
-    m2.run(6)
+    m3 = Diffusion3D(dtype=torch.float64)
+    m1.run(7)
+    m2.run(7)
+    m3.step()
+    m3.capture()  # epoch lives on the device: replays are valid exchanges
+    m3.run(6)
     torch.cuda.synchronize()
     assert torch.equal(m1.T, m2.T)
-    with pytest.raises(Exception, match="cannot be captured"):
-        m1.capture()
+    assert torch.equal(m1.T, m3.T)
+    mesh = H._loopback_comm.mesh
+    mesh.check_error()
+    assert mesh.epoch >= 3 + 3 * 7
     igg.finalize_global_grid(finalize_MPI=False)
