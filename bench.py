@@ -10,10 +10,17 @@ per-N values). ``value`` is the WHOLE-JOB aggregate T_eff (sum over GPUs).
 
 One process per GPU (torchrun); each rank owns a 512^3 block; the process
 topology comes from init_global_grid (2 GPUs -> 2x1x1, 4 -> 2x2x1,
-8 -> 2x2x2); every step = fused stencil + update_halo_ (overlapped).
+8 -> 2x2x2); every step = fused stencil + update_halo_ (serial by default:
+on MI355X the boundary/interior split costs more than the ~40 us exchange).
+
+Multi-GPU: ``--transport auto`` (default) checks that the one-sided put
+transport reproduces the RCCL exchange bitwise on this node, times a few steps
+with each (MAX over ranks) during warm-up and keeps the faster; the timed
+steps are replayed from a hipGraph (two steps per replay) unless --no-graph.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n 512]
                        [--dtype float64] [--overlap] [--variant V|auto]
+                       [--transport auto|rccl|put] [--no-graph]
 """
 from __future__ import annotations
 
@@ -33,16 +40,77 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", type=int, default=512, help="local grid points per dimension")
+    ap.add_argument("--n", "--local-n", dest="n", type=int, default=512, help="local grid points per dimension")
     ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
     ap.add_argument("--overlap", action="store_true", help="boundary/interior split with the halo on a second stream")
     ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
     ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
     ap.add_argument("--loopback", action="store_true",
                     help="1 GPU: route all 6 faces through the RCCL remote path to itself (interior-rank emulation)")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step as a hipGraph (two captured steps per replay)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="replay the step as a hipGraph (two captured steps per replay; default)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "put"],
+                    help="device transport of the halo exchange (multi-GPU / loopback)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: every rank on device 0, 'staged' instead of RCCL as the A/B reference")
     return ap.parse_args()
+
+
+def _max_over_ranks(comm, v: float) -> float:
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.float64)
+    if comm.size > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=comm.gloo)
+    return float(t.item())
+
+
+def _timed(model, comm, k: int) -> float:
+    import torch
+
+    torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        model.step()
+    torch.cuda.synchronize()
+    return _max_over_ranks(comm, time.perf_counter() - t0) / k
+
+
+def select_transport(model, comm, log, ref: str = "rccl") -> tuple[str, dict]:
+    """Bitwise cross-check put vs ``ref`` on the model's field, then A/B timing."""
+    import torch
+
+    from igg.parallel import halo as H
+
+    A, B = model.T.clone(), model.T.clone()
+    H.set_transport(ref)
+    H.update_halo_(A)
+    H.set_transport("put")
+    H.update_halo_(B)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(A, B))
+    try:
+        H.check_transport()
+    except Exception as e:  # a bounded spin timed out: the put path does not work here
+        log(f"put transport failed its check: {e}")
+        comm.mesh.clear_error()
+        ok = False
+    bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
+    del A, B
+    times = {}
+    cands = [ref] + (["put"] if bad == 0.0 else [])
+    for t in cands:
+        H.set_transport(t)
+        model.step()
+        times[t] = _timed(model, comm, 10)
+    best = min(times, key=times.get)
+    H.set_transport(best)
+    log(f"transport A/B (ms/step): {', '.join(f'{k}={v * 1e3:.4f}' for k, v in times.items())}"
+        f"{'' if bad == 0.0 else ' (put mismatched rccl: excluded)'} -> {best}")
+    return best, {k: round(v * 1e3, 5) for k, v in times.items()}
 
 
 def main():
@@ -57,20 +125,36 @@ def main():
 
     if args.variant is not None:
         os.environ["IGG_STENCIL_VARIANT"] = str(args.variant)
+    from igg.parallel import halo as H
+
     dtype = getattr(torch, args.dtype)
     n = args.n
     per = 1 if args.periodic else 0
+    if args.transport != "auto":
+        os.environ["IGG_TRANSPORT"] = args.transport
+    # A put exchange that cannot complete must not stall the run for long.
+    os.environ.setdefault("IGG_PUT_TIMEOUT", "20")
+    if args.share_gpu:
+        os.environ.setdefault("IGG_TRANSPORT", "staged")
     me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, n, periodx=per, periody=per, periodz=per,
-                                                         quiet=True)
+                                                         quiet=True, select_device=not args.share_gpu)
+    log = (lambda m: print(m, file=sys.stderr, flush=True)) if me == 0 else (lambda m: None)
     if args.loopback:
-        from igg.parallel.halo import enable_loopback
-
-        enable_loopback()
+        H.enable_loopback()
     model = Diffusion3D(dtype=dtype, overlap=args.overlap)
+    ab = None
+    if nprocs > 1 and args.transport == "auto":
+        _, ab = select_transport(model, comm, log, ref="staged" if args.share_gpu else "rccl")
     for _ in range(args.warmup):
         model.step()
+    graph_error = None
     if args.graph:
-        model.capture()
+        try:
+            model.capture()
+        except Exception as e:  # capture unsupported here: time eager steps
+            graph_error = f"{type(e).__name__}: {e}"[:200]
+            model.graph = None
+            log(f"hipGraph capture failed, running eager: {graph_error}")
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -79,14 +163,8 @@ def main():
     torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    # MAX over ranks (gloo all-reduce of one double)
-    el = torch.tensor([elapsed], dtype=torch.float64)
-    if nprocs > 1:
-        import torch.distributed as dist
-
-        dist.all_reduce(el, op=dist.ReduceOp.MAX, group=comm.gloo)
-    elapsed = float(el.item())
+    elapsed = _max_over_ranks(comm, t1 - t0)
+    H.check_transport()
     t_it = elapsed / args.steps
     per_gpu = t_eff_gbs(model, t_it)
     total = per_gpu * nprocs
@@ -115,11 +193,13 @@ def main():
                 "overlap_comm": bool(model.overlap),
                 "t_eff_per_gpu_GBs": round(per_gpu, 3),
                 "a_eff_bytes_per_gpu": model.a_eff_bytes,
-                "transport": os.environ.get("IGG_TRANSPORT", "rccl") if nprocs > 1 else "none",
+                "transport": H.transport_name(),
+                "transport_ab_ms": ab,
                 "stencil_variant": os.environ.get("IGG_STENCIL_VARIANT", "0"),
                 "finite": finite,
                 "loopback_emulation": bool(args.loopback),
                 "hip_graph": model.graph is not None,
+                "hip_graph_error": graph_error,
             },
         }
         print(json.dumps(out), flush=True)

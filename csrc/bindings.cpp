@@ -288,6 +288,7 @@ PYBIND11_MODULE(_igg_native, m) {
       .def_property_readonly("flag_words", &PeerMesh::flag_words)
       .def("flag", &PeerMesh::read_flag)
       .def("check_error", &PeerMesh::check_error)
+      .def("clear_error", &PeerMesh::clear_error)
       .def("close", &PeerMesh::close);
   py::class_<PutTransport, Transport, std::shared_ptr<PutTransport>>(m, "PutTransport")
       .def(py::init<std::shared_ptr<PeerMesh>>(), py::arg("mesh"))

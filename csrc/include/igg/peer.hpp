@@ -50,6 +50,7 @@ class PeerMesh {
   uint64_t read_flag(int idx) const;
   // Raises igg::Error if a put-transport kernel timed out waiting for a peer.
   void check_error() const;
+  void clear_error();
   int64_t timeout_ticks() const { return timeout_ticks_; }
   // Collective teardown (also run by the destructor without the collectives).
   void close();

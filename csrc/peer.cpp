@@ -38,6 +38,12 @@ void PeerMesh::check_error() const {
          "legitimately slow.");
 }
 
+void PeerMesh::clear_error() {
+  if (!flags_) return;
+  IGG_HIP_CHECK(hipMemsetAsync(flags_ + PutFlags::ERROR, 0, 8, side_));
+  IGG_HIP_CHECK(hipStreamSynchronize(side_));
+}
+
 PeerMesh::~PeerMesh() {
   // Non-collective fallback: unmap peers, free own memory (the collective
   // close() should have run first; by then these are no-ops).

@@ -142,10 +142,14 @@ class Communicator:
             self._transports["gloo"] = t
         return t
 
-    def device_transport(self):
+    def device_transport(self, choice: str | None = None):
+        """Device transport ``choice`` (default: ``IGG_TRANSPORT``), created once
+        and cached; creating the RCCL communicator or the put mesh is collective."""
         if self.size == 1:
             return None
-        choice = config.transport_choice()
+        choice = config.transport_choice() if choice is None else choice
+        if choice not in ("rccl", "torch", "staged", "put"):
+            raise IGGError(f"unknown device transport {choice!r}")
         if choice == "staged":
             t = self._transports.get("staged")
             if t is None:

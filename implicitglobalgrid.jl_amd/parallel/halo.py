@@ -147,6 +147,24 @@ def _drop_engine() -> None:
     _loopback_comm = None
 
 
+def set_transport(name: str) -> None:
+    """Switch the device transport of ``update_halo_`` ('rccl', 'put', 'torch'
+    or 'staged'). Collective: every rank must switch at the same point (the
+    first use of a transport creates its communicator / peer mesh)."""
+    gg = _grid.global_grid()
+    if gg.nprocs == 1:
+        raise IGGError("set_transport: a single-process grid has no device transport")
+    if not gg.amdgpu_enabled:
+        raise IGGError("set_transport: the grid was not initialised for GPU fields")
+    _engine.set_transport(gg.comm.device_transport(name), True)
+
+
+def transport_name() -> str:
+    """Name of the device transport update_halo_ currently uses ('none' if single-process)."""
+    _grid.check_initialized()
+    return _engine.transport_name(True)
+
+
 def check_transport() -> None:
     """Raise if a put-transport synchronisation kernel timed out (its spin
     waits are bounded; a timeout means some exchange's halo is invalid)."""
