@@ -33,6 +33,16 @@ import time
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
+# BASELINE.json configs. The driver runs the default (the headline metric).
+CONFIGS = {
+    "diffusion3d": dict(model="diffusion3d", n=512, dtype="float64", gather_every=0, metric=METRIC),
+    "diffusion3d_f32_gather": dict(
+        model="diffusion3d", n=1024, dtype="float32", gather_every=100,
+        metric="effective GB/s per GPU, 3-D diffusion 1024^3/GPU Float32 with gather_ every 100 steps"),
+    "acoustic2d": dict(
+        model="acoustic2d", n=8192, dtype="float32", gather_every=0,
+        metric="effective GB/s per GPU, 2-D staggered acoustic solver 8192^2/GPU Float32"),
+}
 
 
 def parse():
@@ -40,8 +50,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", "--local-n", dest="n", type=int, default=512, help="local grid points per dimension")
-    ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--config", default="diffusion3d", choices=sorted(CONFIGS))
+    ap.add_argument("--n", "--local-n", dest="n", type=int, default=None,
+                    help="local grid points per dimension (default: per config)")
+    ap.add_argument("--dtype", default=None, choices=["float64", "float32"])
+    ap.add_argument("--gather-every", type=int, default=None, help="gather_ the field to rank 0 every K steps")
     ap.add_argument("--overlap", action="store_true", help="boundary/interior split with the halo on a second stream")
     ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
     ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
@@ -79,13 +92,13 @@ def _timed(model, comm, k: int) -> float:
     return _max_over_ranks(comm, time.perf_counter() - t0) / k
 
 
-def select_transport(model, comm, log, ref: str = "rccl") -> tuple[str, dict]:
+def select_transport(model, field, comm, log, ref: str = "rccl") -> tuple[str, dict]:
     """Bitwise cross-check put vs ``ref`` on the model's field, then A/B timing."""
     import torch
 
     from igg.parallel import halo as H
 
-    A, B = model.T.clone(), model.T.clone()
+    A, B = field.clone(), field.clone()
     H.set_transport(ref)
     H.update_halo_(A)
     H.set_transport("put")
@@ -121,14 +134,18 @@ def main():
     import torch
 
     import igg
-    from igg.models.diffusion3d import Diffusion3D, t_eff_gbs
+    from igg.models.acoustic2d import Acoustic2D
+    from igg.models.diffusion3d import Diffusion3D
 
     if args.variant is not None:
         os.environ["IGG_STENCIL_VARIANT"] = str(args.variant)
     from igg.parallel import halo as H
 
-    dtype = getattr(torch, args.dtype)
-    n = args.n
+    cfg = CONFIGS[args.config]
+    dtype = getattr(torch, args.dtype or cfg["dtype"])
+    n = args.n or cfg["n"]
+    gather_every = cfg["gather_every"] if args.gather_every is None else args.gather_every
+    is2d = cfg["model"] == "acoustic2d"
     per = 1 if args.periodic else 0
     if args.transport != "auto":
         os.environ["IGG_TRANSPORT"] = args.transport
@@ -136,15 +153,21 @@ def main():
     os.environ.setdefault("IGG_PUT_TIMEOUT", "20")
     if args.share_gpu:
         os.environ.setdefault("IGG_TRANSPORT", "staged")
-    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, n, periodx=per, periody=per, periodz=per,
-                                                         quiet=True, select_device=not args.share_gpu)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, 1 if is2d else n, periodx=per, periody=per,
+                                                         periodz=0 if is2d else per, quiet=True,
+                                                         select_device=not args.share_gpu)
     log = (lambda m: print(m, file=sys.stderr, flush=True)) if me == 0 else (lambda m: None)
     if args.loopback:
-        H.enable_loopback()
-    model = Diffusion3D(dtype=dtype, overlap=args.overlap)
+        H.enable_loopback((True, True, not is2d))
+    model = Acoustic2D(dtype=dtype) if is2d else Diffusion3D(dtype=dtype, overlap=args.overlap)
+    field = (lambda: model.P) if is2d else (lambda: model.T)
+    A_global = None
+    if gather_every > 0 and me == 0:
+        A_global = torch.empty([int(v) for v in igg.get_global_grid().nxyz_g][: 2 if is2d else 3],
+                               dtype=dtype, device=field().device)
     ab = None
     if nprocs > 1 and args.transport == "auto":
-        _, ab = select_transport(model, comm, log, ref="staged" if args.share_gpu else "rccl")
+        _, ab = select_transport(model, field(), comm, log, ref="staged" if args.share_gpu else "rccl")
     for _ in range(args.warmup):
         model.step()
     graph_error = None
@@ -159,19 +182,36 @@ def main():
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    model.run(args.steps)
+    if gather_every > 0:
+        done = 0
+        while done < args.steps:
+            k = min(gather_every, args.steps - done)
+            model.run(k)
+            done += k
+            if done % gather_every == 0:
+                igg.gather_(field(), A_global)
+    else:
+        model.run(args.steps)
     torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
     elapsed = _max_over_ranks(comm, t1 - t0)
     H.check_transport()
     t_it = elapsed / args.steps
-    per_gpu = t_eff_gbs(model, t_it)
+    per_gpu = model.a_eff_bytes / t_it / 1e9
     total = per_gpu * nprocs
-    finite = bool(torch.isfinite(model.T).all().item())
+    finite = bool(torch.isfinite(field()).all().item())
+    gather_ms = None
+    if gather_every > 0:
+        torch.cuda.synchronize()
+        comm.barrier()
+        tg = time.perf_counter()
+        igg.gather_(field(), A_global)
+        torch.cuda.synchronize()
+        gather_ms = round(_max_over_ranks(comm, time.perf_counter() - tg) * 1e3, 3)
     if me == 0:
         out = {
-            "metric": METRIC,
+            "metric": cfg["metric"],
             "value": round(total, 3),
             "unit": "GB/s",
             "n_gpus": nprocs,
@@ -180,17 +220,20 @@ def main():
             "ms_per_step": round(t_it * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(per_gpu / BASELINE_PER_GPU_GBS, 3),
+            "vs_baseline": round(per_gpu / BASELINE_PER_GPU_GBS, 3) if args.config == "diffusion3d" else None,
             "dtype": "fp64" if dtype == torch.float64 else "fp32",
             "data": "synthetic (Gaussian-anomaly initial conditions, reference example physics)",
             "config": {
-                "model": "diffusion3d",
+                "model": cfg["model"],
+                "bench_config": args.config,
                 "global_batch": nprocs,
                 "seq_len": n,
                 "parallelism": f"spatial {dims[0]}x{dims[1]}x{dims[2]}",
-                "local_grid": [n, n, n],
+                "local_grid": [n, n] if is2d else [n, n, n],
                 "global_grid": [int(v) for v in igg.get_global_grid().nxyz_g],
-                "overlap_comm": bool(model.overlap),
+                "overlap_comm": bool(getattr(model, "overlap", False)),
+                "gather_every": gather_every,
+                "gather_ms": gather_ms,
                 "t_eff_per_gpu_GBs": round(per_gpu, 3),
                 "a_eff_bytes_per_gpu": model.a_eff_bytes,
                 "transport": H.transport_name(),

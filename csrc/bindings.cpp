@@ -9,6 +9,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "igg/acoustic.hpp"
 #include "igg/comm.hpp"
 #include "igg/copy.hpp"
 #include "igg/gather.hpp"
@@ -396,6 +397,21 @@ PYBIND11_MODULE(_igg_native, m) {
     launch_stream_probe(kind, reinterpret_cast<double*>(out), reinterpret_cast<const double*>(a),
                         reinterpret_cast<const double*>(b), n, blocks, as_stream(stream));
   });
+  m.def("acoustic2d",
+        [](uintptr_t p2, uintptr_t vx2, uintptr_t vy2, uintptr_t p, uintptr_t vx, uintptr_t vy, int64_t nx,
+           int64_t ny, double dtk, double dt_rho, double rdx, double rdy, int elem_bytes, bool device,
+           uintptr_t stream) {
+          AcousticArgs a{p2, vx2, vy2, p, vx, vy, nx, ny, dtk, dt_rho, rdx, rdy, elem_bytes};
+          if (device) {
+            launch_acoustic2d(a, as_stream(stream));
+          } else {
+            py::gil_scoped_release nogil;
+            host_acoustic2d(a);
+          }
+        },
+        py::arg("p2"), py::arg("vx2"), py::arg("vy2"), py::arg("p"), py::arg("vx"), py::arg("vy"), py::arg("nx"),
+        py::arg("ny"), py::arg("dtk"), py::arg("dt_rho"), py::arg("rdx"), py::arg("rdy"), py::arg("elem_bytes"),
+        py::arg("device"), py::arg("stream") = 0);
   m.def("diffusion3d_set_rounds", &diffusion3d_set_rounds);
   m.def("diffusion3d_get_rounds", &diffusion3d_get_rounds);
   m.def("diffusion3d",

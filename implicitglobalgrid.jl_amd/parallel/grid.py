@@ -22,7 +22,8 @@ from . import comm as _comm
 DEVICE_TYPE_AUTO = "auto"
 DEVICE_TYPE_CUDA = "CUDA"
 DEVICE_TYPE_AMDGPU = "AMDGPU"
-_DEVICE_TYPES = (DEVICE_TYPE_AUTO, DEVICE_TYPE_CUDA, DEVICE_TYPE_AMDGPU)
+DEVICE_TYPE_NONE = "none"  # extension: host (CPU) fields only, even on a GPU node
+_DEVICE_TYPES = (DEVICE_TYPE_AUTO, DEVICE_TYPE_CUDA, DEVICE_TYPE_AMDGPU, DEVICE_TYPE_NONE)
 
 
 def _i3(v=-1):
