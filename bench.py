@@ -238,7 +238,8 @@ def main():
                 "a_eff_bytes_per_gpu": model.a_eff_bytes,
                 "transport": H.transport_name(),
                 "transport_ab_ms": ab,
-                "stencil_variant": os.environ.get("IGG_STENCIL_VARIANT", "0"),
+                "stencil_variant": getattr(model, "variant", None),
+                "stencil_variant_ms": getattr(model, "variant_times", None),
                 "finite": finite,
                 "loopback_emulation": bool(args.loopback),
                 "hip_graph": model.graph is not None,

@@ -412,6 +412,8 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("p2"), py::arg("vx2"), py::arg("vy2"), py::arg("p"), py::arg("vx"), py::arg("vy"), py::arg("nx"),
         py::arg("ny"), py::arg("dtk"), py::arg("dt_rho"), py::arg("rdx"), py::arg("rdy"), py::arg("elem_bytes"),
         py::arg("device"), py::arg("stream") = 0);
+  m.def("acoustic2d_set_variant", &acoustic2d_set_variant);
+  m.def("acoustic2d_set_chunk", &acoustic2d_set_chunk);
   m.def("diffusion3d_set_rounds", &diffusion3d_set_rounds);
   m.def("diffusion3d_get_rounds", &diffusion3d_get_rounds);
   m.def("diffusion3d",

@@ -31,6 +31,9 @@ struct AcousticArgs {
 };
 
 void launch_acoustic2d(const AcousticArgs& a, hipStream_t stream);
+// 0: one thread per cell with neighbour recomputation, 1 (default): marching.
+void acoustic2d_set_variant(int v);
+void acoustic2d_set_chunk(int64_t rows);  // rows of i per wave of the marching kernel
 void host_acoustic2d(const AcousticArgs& a);
 
 }  // namespace igg

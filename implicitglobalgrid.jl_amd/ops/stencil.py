@@ -55,24 +55,38 @@ def _variant_for(T, boxes, rd2, dtlam, T2, Cp, stream) -> int:
     return v
 
 
-def autotune(T2, T, Cp, rd2, dtlam, boxes, reps: int = 5) -> int:
-    """Time every kernel variant on these arrays (the update is pure: T2 = f(T, Cp))."""
+# Variants that win somewhere on MI355X (sweeps in profiles/): v4_by4_ry4_nt,
+# v2_by4_ry4_pf_nt, v4_by4_ry4, v4_by4_ry8_nt, v2_by4_ry8_nt, v4_bz2_by2_ry8_nt.
+SHORTLIST = (0, 2, 3, 9, 11, 14)
+
+
+def time_variants(T2, T, Cp, rd2, dtlam, boxes, candidates=None, reps: int = 5, rounds: int = 3) -> dict:
+    """Median-of-rounds time (ms) of each candidate variant on these arrays,
+    interleaved (the update is pure: T2 = f(T, Cp), so T2 can be scribbled)."""
     n = list(T.shape)
-    best, best_t = 0, float("inf")
+    cands = list(range(len(variants()))) if candidates is None else list(candidates)
     s = torch.cuda.current_stream()
-    for v in range(len(variants())):
-        args = (T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(), boxes, True, v, s.cuda_stream)
-        native.diffusion3d(*args)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
-            native.diffusion3d(*args)
-        e1.record(s)
-        e1.synchronize()
-        t = e0.elapsed_time(e1)
-        if t < best_t:
-            best, best_t = v, t
-    return best
+    times = {v: [] for v in cands}
+    for v in cands:  # warm every code object once
+        native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(), boxes, True,
+                           v, s.cuda_stream)
+    for _ in range(rounds):
+        for v in cands:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(),
+                                   boxes, True, v, s.cuda_stream)
+            e1.record(s)
+            e1.synchronize()
+            times[v].append(e0.elapsed_time(e1) / reps)
+    return {v: sorted(t)[len(t) // 2] for v, t in times.items()}
+
+
+def autotune(T2, T, Cp, rd2, dtlam, boxes, reps: int = 5, candidates=None) -> int:
+    """Fastest variant on these arrays (this process only)."""
+    t = time_variants(T2, T, Cp, rd2, dtlam, boxes, candidates, reps)
+    return min(t, key=t.get)
 
 
 def diffusion3d_(T2, T, Cp, *, lam: float, dt: float, dx: float, dy: float, dz: float,

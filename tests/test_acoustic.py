@@ -60,11 +60,17 @@ def test_multirank_matches_global(nprocs):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-13), (torch.float32, 2e-6)])
-def test_gpu_step_matches_reference(gpu, dtype, tol):
-    P, Vx, Vy = _fields(130, 257, dtype, gpu)
-    got = _step(P, Vx, Vy, True, **KW)
-    torch.cuda.synchronize()
+@pytest.mark.parametrize("shape", [(130, 257), (64, 63), (200, 64), (3, 2)])
+def test_gpu_step_matches_reference(gpu, variant, dtype, tol, shape):
+    P, Vx, Vy = _fields(*shape, dtype, gpu)
+    native.acoustic2d_set_variant(variant)
+    try:
+        got = _step(P, Vx, Vy, True, **KW)
+        torch.cuda.synchronize()
+    finally:
+        native.acoustic2d_set_variant(1)
     ref = acoustic2d_reference(P.cpu(), Vx.cpu(), Vy.cpu(), **KW)
     for g, r in zip(got, ref):
         assert (g.cpu().double() - r).abs().max().item() < tol
