@@ -201,6 +201,16 @@ def main():
     per_gpu = model.a_eff_bytes / t_it / 1e9
     total = per_gpu * nprocs
     finite = bool(torch.isfinite(field()).all().item())
+    phase_ms = None
+    if not is2d and nprocs > 1 or args.loopback:
+        # stencil vs halo split of a few eager steps (events on the stream)
+        from igg.utils.trace import PhaseTimer
+
+        model.timer = PhaseTimer()
+        for _ in range(10):
+            model.step()
+        phase_ms = {k: v["mean_ms"] for k, v in model.timer.summary().items()}
+        model.timer = None
     gather_ms = None
     if gather_every > 0:
         torch.cuda.synchronize()
@@ -234,6 +244,7 @@ def main():
                 "overlap_comm": bool(getattr(model, "overlap", False)),
                 "gather_every": gather_every,
                 "gather_ms": gather_ms,
+                "phase_ms": phase_ms,
                 "t_eff_per_gpu_GBs": round(per_gpu, 3),
                 "a_eff_bytes_per_gpu": model.a_eff_bytes,
                 "transport": H.transport_name(),

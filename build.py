@@ -92,7 +92,7 @@ def build(jobs: int | None = None, debug: bool = False, asan: bool = False, verb
         link = [
             str(ROCM / "bin" / "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}",
             *map(str, objs), "-o", str(out) + ".tmp",
-            f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}",
+            f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64", "-ldl", f"-Wl,-rpath,{ROCM / 'lib'}",
         ]
         if asan:
             link += ["-fsanitize=address"]

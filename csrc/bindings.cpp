@@ -17,6 +17,7 @@
 #include "igg/ipc.hpp"
 #include "igg/stencil.hpp"
 #include "igg/topology.hpp"
+#include "igg/trace.hpp"
 
 namespace igg {
 void launch_stream_probe(int kind, double* out, const double* a, const double* b, int64_t n, int blocks,
@@ -158,6 +159,10 @@ PYBIND11_MODULE(_igg_native, m) {
     return py::bytes(out);
   });
   m.def("rccl_version", &rccl_version);
+  m.def("trace_enabled", &trace_enabled);
+  m.def("trace_push", [](const std::string& n) { trace_push(n.c_str()); });
+  m.def("trace_pop", &trace_pop);
+  m.def("trace_mark", [](const std::string& n) { trace_mark(n.c_str()); });
 
   // --- intra-node peer memory (put transport primitives)
   m.def("ipc_malloc", [](size_t bytes, int kind) {
@@ -401,6 +406,7 @@ PYBIND11_MODULE(_igg_native, m) {
         [](uintptr_t p2, uintptr_t vx2, uintptr_t vy2, uintptr_t p, uintptr_t vx, uintptr_t vy, int64_t nx,
            int64_t ny, double dtk, double dt_rho, double rdx, double rdy, int elem_bytes, bool device,
            uintptr_t stream) {
+          TraceRange tr("igg.acoustic2d");
           AcousticArgs a{p2, vx2, vy2, p, vx, vy, nx, ny, dtk, dt_rho, rdx, rdy, elem_bytes};
           if (device) {
             launch_acoustic2d(a, as_stream(stream));
@@ -420,6 +426,7 @@ PYBIND11_MODULE(_igg_native, m) {
         [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
            double dtlam, int elem_bytes, const std::vector<std::pair<Int3, Int3>>& boxes,
            bool device, int variant, uintptr_t stream, int rounds) {
+          TraceRange tr("igg.diffusion3d");
           DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes, rounds};
           const auto bx = to_boxes(boxes);
           if (device) {

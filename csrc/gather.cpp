@@ -1,5 +1,6 @@
 // Device gather-to-root (see include/igg/gather.hpp).
 #include "igg/gather.hpp"
+#include "igg/trace.hpp"
 
 #include <hip/hip_runtime_api.h>
 
@@ -16,6 +17,7 @@ void Gatherer::free() {
 
 void Gatherer::gather(const Field& a, void* dst, int root, const Int3& dims, RcclComm& comm,
                       hipStream_t stream) {
+  TraceRange tr("igg.gather");
   if (!a.device) fail("Gatherer: the local array must be a GPU array.");
   const int64_t len = a.size[0] * a.size[1] * a.size[2];
   const size_t blk = static_cast<size_t>(len) * a.elem_bytes;

@@ -1,6 +1,7 @@
 // Halo exchange engine (see include/igg/halo.hpp for the behavioural contract).
 #include "igg/halo.hpp"
 #include "igg/ipc.hpp"
+#include "igg/trace.hpp"
 
 #include <unistd.h>
 
@@ -184,6 +185,7 @@ HaloEngine::~HaloEngine() {
 
 void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) {
   if (fields.empty()) return;
+  TraceRange tr("igg.update_halo");
   const bool device = fields[0].device;
   bool capturing = false;
   if (device) {
@@ -306,8 +308,18 @@ void HaloEngine::exchange_dim_impl(const std::vector<Field>& fields, int dim, bo
                        static_cast<int>(i * 2 + (1 - s))});
     }
   }
-  do_copies(pack);
-  transport_->exchange(recvs, sends, device, stream);
+  static const char* const kPack[3] = {"igg.seq.pack.x", "igg.seq.pack.y", "igg.seq.pack.z"};
+  static const char* const kComm[3] = {"igg.seq.transport.x", "igg.seq.transport.y", "igg.seq.transport.z"};
+  static const char* const kUnpack[3] = {"igg.seq.unpack.x", "igg.seq.unpack.y", "igg.seq.unpack.z"};
+  {
+    TraceRange r(kPack[dim]);
+    do_copies(pack);
+  }
+  {
+    TraceRange r(kComm[dim]);
+    transport_->exchange(recvs, sends, device, stream);
+  }
+  TraceRange r(kUnpack[dim]);
   do_copies(unpack);
 }
 
@@ -455,10 +467,22 @@ void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stre
   for (int j = 0; j < ps.n_nb; ++j) ps.nb_flags[j] = mesh.flags(nb_ranks[j]);
   const uint64_t* epoch = mesh.flags(me) + PutFlags::EPOCH;
   // begin -> put (stores into the receivers' arenas) -> sync -> unpack
-  launch_put_begin(ps, stream);
-  launch_copy2d(put, eb, stream, /*system_fence=*/true, ParityShift{epoch, half, 1});
-  launch_put_sync(ps, stream);
-  launch_copy2d(unpack, eb, stream, false, ParityShift{epoch, half, 2});
+  {
+    TraceRange r("igg.put.begin");
+    launch_put_begin(ps, stream);
+  }
+  {
+    TraceRange r("igg.put.pack");
+    launch_copy2d(put, eb, stream, /*system_fence=*/true, ParityShift{epoch, half, 1});
+  }
+  {
+    TraceRange r("igg.put.sync");
+    launch_put_sync(ps, stream);
+  }
+  {
+    TraceRange r("igg.put.unpack");
+    launch_copy2d(unpack, eb, stream, false, ParityShift{epoch, half, 2});
+  }
   static const bool debug = std::getenv("IGG_PUT_DEBUG") != nullptr;
   if (debug) {
     IGG_HIP_CHECK(hipStreamSynchronize(stream));
@@ -545,7 +569,10 @@ void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device
     if (m.peer == g.me) self_src[m.field * 27 + m.key] = dst;
     else tsend.push_back({dst, fc.bytes, static_cast<int>(m.peer), static_cast<int>(m.field * 27 + m.key)});
   }
-  do_copies(pack);
+  {
+    TraceRange r("igg.onephase.pack");
+    do_copies(pack);
+  }
   // 2. one communication phase for all remote messages
   std::vector<Copy2D> unpack;
   for (const Msg& m : recvs) {
@@ -562,8 +589,12 @@ void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device
     }
     unpack.push_back({src, fc.base, fc.n_outer, fc.n_inner, fc.n_inner, 1, fc.s_outer, fc.s_inner});
   }
-  if (!tsend.empty() || !trecv.empty()) tr->exchange(trecv, tsend, device, stream);
+  if (!tsend.empty() || !trecv.empty()) {
+    TraceRange r("igg.onephase.transport");
+    tr->exchange(trecv, tsend, device, stream);
+  }
   // 3. unpack every receive region (disjoint: one launch)
+  TraceRange r3("igg.onephase.unpack");
   do_copies(unpack);
 }
 

@@ -48,6 +48,7 @@ class Diffusion3D:
         self.dt = min(self.dx ** 2, self.dy ** 2, self.dz ** 2) * cp_min / lam / 8.1
         self.variant = variant
         self.variant_times = None  # per-variant ms when autotuned (see _choose_variant)
+        self.timer = None  # optional utils.trace.PhaseTimer (eager steps only)
         # Overlap tuning knobs: kernel variant / grid rounds of the boundary
         # slabs and grid rounds of the interior launch (see ops.stencil).
         self.halo_variant = halo_variant
@@ -126,6 +127,11 @@ class Diffusion3D:
             main.wait_stream(hs)
             if cs is not main:
                 main.wait_stream(cs)
+        elif self.timer is not None:
+            with self.timer.phase("stencil"):
+                stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
+            with self.timer.phase("update_halo"):
+                update_halo_(T2)
         else:
             stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
             update_halo_(T2)

@@ -167,7 +167,8 @@ def transport_name() -> str:
 
 def check_transport() -> None:
     """Raise if a put-transport synchronisation kernel timed out (its spin
-    waits are bounded; a timeout means some exchange's halo is invalid)."""
+    waits are bounded; a timeout means some exchange's halo is invalid) or an
+    RCCL communicator reported an asynchronous error."""
     meshes = []
     gg = _grid.global_grid()
     if gg.comm is not None and getattr(gg.comm, "mesh", None) is not None:
@@ -176,6 +177,12 @@ def check_transport() -> None:
         meshes.append(_loopback_comm.mesh)
     for m in meshes:
         m.check_error()
+    rcc = [getattr(gg.comm, "rccl", None) if gg.comm is not None else None]
+    if _loopback_comm is not None and isinstance(_loopback_comm, native.RcclComm):
+        rcc.append(_loopback_comm)
+    for c in rcc:
+        if c is not None:
+            c.check_async_error()  # ncclCommGetAsyncError: raises on an asynchronous RCCL failure
 
 
 def engine():
