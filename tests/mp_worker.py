@@ -163,6 +163,65 @@ def scenario_acoustic(dev, nx, ny, steps):
     print(f"rank {me} acoustic OK dims={dims.tolist()}")
 
 
+def scenario_put_timeout():
+    """Rank 1 skips one update_halo_: rank 0's bounded waits expire (short
+    IGG_PUT_TIMEOUT), its kernels exit, and check_transport reports it."""
+    import time
+
+    from igg.parallel import halo as H
+
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 6, 5, periodx=1, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    A = torch.zeros(8, 6, 5, dtype=torch.float64, device="cuda")
+    igg.update_halo_(A)  # a healthy exchange first
+    torch.cuda.synchronize()
+    H.check_transport()
+    comm.barrier()
+    if me == 0:
+        t0 = time.time()
+        igg.update_halo_(A)
+        torch.cuda.synchronize()  # returns once the spin times out (no hang)
+        waited = time.time() - t0
+        try:
+            H.check_transport()
+            raise AssertionError("expected a put-transport timeout error")
+        except igg.IGGError as e:
+            assert "timed out" in str(e)
+        assert waited >= 1.0, waited
+        comm.mesh.clear_error()
+    comm.barrier()
+    igg.finalize_global_grid()
+    print(f"rank {me} put timeout OK")
+
+
+def scenario_put_skew(steps):
+    """Ranks reach the exchanges at very different times (random host sleeps):
+    the device-side waits absorb the skew and every halo stays exact."""
+    import random
+    import time
+
+    steps = int(steps)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(7, 5, 6, periodx=1, periody=1, periodz=1, quiet=True,
+                                                          select_device=False, device_type="AMDGPU")
+    gg = igg.get_global_grid()
+    rng = random.Random(1234 + me)
+    A = torch.zeros(7, 5, 6, dtype=torch.float64)
+    encode(A)
+    ref = expected_after_halo(A, has_halo(A, gg), gg.neighbors.tolist())
+    X = zero_boundaries(A.clone()).to("cuda")
+    for k in range(steps):
+        time.sleep(rng.random() * 0.05)
+        X = zero_boundaries(X.cpu()).to("cuda") if k % 3 == 0 else X
+        igg.update_halo_(X)
+    got = X.cpu()
+    assert torch.equal(got, ref), f"rank {me}: halo mismatch after skewed exchanges"
+    from igg.parallel import halo as H
+
+    H.check_transport()
+    igg.finalize_global_grid()
+    print(f"rank {me} put skew OK")
+
+
 def scenario_ring(dev):
     """Transport-level ring exchange (test_update_halo.jl:697-743 analogue)."""
     device = _device(dev)

@@ -89,3 +89,13 @@ def test_halo_gpu_multirank_put(nprocs, cfg):
 @pytest.mark.parametrize("overlap", [0, 1])
 def test_diffusion_gpu_multirank_put(overlap):
     run_ranks(8, "diffusion", "gpu", 24, 20, 18, 7, overlap, env_extra=PUT_ENV)
+
+
+@pytest.mark.gpu
+def test_put_transport_timeout_reports_and_never_hangs():
+    run_ranks(2, "put_timeout", env_extra={**PUT_ENV, "IGG_PUT_TIMEOUT": "2"}, timeout=120)
+
+
+@pytest.mark.gpu
+def test_put_transport_absorbs_rank_skew():
+    run_ranks(4, "put_skew", 12, env_extra=PUT_ENV, timeout=200)
