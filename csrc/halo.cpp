@@ -466,14 +466,19 @@ void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stre
   for (int j = 0; j < ps.n_in; ++j) ps.in_rank[j] = in_ranks[j];
   for (int j = 0; j < ps.n_nb; ++j) ps.nb_flags[j] = mesh.flags(nb_ranks[j]);
   const uint64_t* epoch = mesh.flags(me) + PutFlags::EPOCH;
-  // begin -> put (stores into the receivers' arenas) -> sync -> unpack
-  {
+  // [begin] -> put (stores into the receivers' arenas) -> sync -> unpack
+  bool implied = put_count_ >= 2;  // exchanges 1 and 2 use fresh halves
+  for (int r : out_ranks)
+    if (std::find(prev_in_.begin(), prev_in_.end(), r) == prev_in_.end()) implied = false;
+  if (!implied && put_count_ >= 2) {
     TraceRange r("igg.put.begin");
     launch_put_begin(ps, stream);
   }
+  ++put_count_;
+  prev_in_ = in_ranks;
   {
     TraceRange r("igg.put.pack");
-    launch_copy2d(put, eb, stream, /*system_fence=*/true, ParityShift{epoch, half, 1});
+    launch_copy2d(put, eb, stream, /*system_fence=*/true, ParityShift{epoch, half, 1, 1});
   }
   {
     TraceRange r("igg.put.sync");
@@ -481,7 +486,7 @@ void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stre
   }
   {
     TraceRange r("igg.put.unpack");
-    launch_copy2d(unpack, eb, stream, false, ParityShift{epoch, half, 2});
+    launch_copy2d(unpack, eb, stream, false, ParityShift{epoch, half, 2, 0});
   }
   static const bool debug = std::getenv("IGG_PUT_DEBUG") != nullptr;
   if (debug) {

@@ -39,12 +39,14 @@ struct CopyBatch {
   const uint64_t* epoch = nullptr;
   int64_t parity_bytes = 0;
   int parity_side = 0;
+  int parity_add = 0;  // half = ((*epoch + parity_add) & 1)
 };
 
 struct ParityShift {
   const uint64_t* epoch = nullptr;
   int64_t bytes = 0;
   int side = 0;  // 0 none, 1 dst, 2 src
+  int add = 0;   // the half is ((*epoch + add) & 1)
 };
 
 // Device: enqueue all copies (any count, split in MAX_BATCH chunks) on `stream`.

@@ -26,7 +26,7 @@ struct alignas(16) B16 { uint64_t x, y; };
 __device__ __forceinline__ int64_t parity_shift(const CopyBatch& b) {
   if (b.parity_side == 0) return 0;
   const uint64_t e = __hip_atomic_load(b.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return (e & 1) ? b.parity_bytes : 0;
+  return ((e + b.parity_add) & 1) ? b.parity_bytes : 0;
 }
 
 template <typename T, bool FENCE>
@@ -83,6 +83,7 @@ void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream, const P
     batch.epoch = par.epoch;
     batch.parity_bytes = par.bytes;
     batch.parity_side = par.side;
+    batch.parity_add = par.add;
     int64_t blocks = 0;
     while (pos < copies.size() && batch.n < MAX_BATCH) {
       const Copy2D& c = copies[pos++];

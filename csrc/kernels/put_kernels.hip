@@ -29,30 +29,33 @@ __device__ bool wait_geq(const uint64_t* p, uint64_t v, const PutSync& s, uint64
   return true;
 }
 
+// The EPOCH word counts completed exchanges (c); exchange e = c + 1.
 __global__ void __launch_bounds__(64) put_begin_kernel(const PutSync s) {
-  __shared__ uint64_t epoch;
   const int lane = threadIdx.x;
-  if (lane == 0) {
-    const uint64_t e = load_sys(s.my_flags + PutFlags::EPOCH) + 1;
-    store_sys(s.my_flags + PutFlags::EPOCH, e);
-    epoch = e;
-  }
-  __syncthreads();
-  const uint64_t e = epoch;
+  const uint64_t e = load_sys(s.my_flags + PutFlags::EPOCH) + 1;
   const int freed = PutFlags::freed(s.nranks);
-  // My unpack of e-1 completed before this kernel started (same stream).
-  if (lane < s.n_nb && e > 1) store_sys(s.nb_flags[lane] + freed + s.my_rank, e - 1);
+  // Each receiver must have finished unpacking exchange e-2 (the last one
+  // that used arena half e&1) before my put kernel writes into it.
   if (lane < s.n_out && e > 2) wait_geq(s.my_flags + freed + s.out_rank[lane], e - 2, s, 0x100 + lane);
 }
 
 __global__ void __launch_bounds__(64) put_sync_kernel(const PutSync s) {
+  __shared__ int ok;
   const int lane = threadIdx.x;
-  const uint64_t e = load_sys(s.my_flags + PutFlags::EPOCH);
-  // The put kernel(s) finished (stream order) with their stores acknowledged;
-  // one system-scope release here orders them before the flag stores.
+  const uint64_t e = load_sys(s.my_flags + PutFlags::EPOCH) + 1;
+  const int freed = PutFlags::freed(s.nranks);
+  if (lane == 0) ok = 1;
+  __syncthreads();
+  // My unpack of e-1 completed before this kernel (stream order): release my
+  // arena half to every neighbour. The put kernel(s) of e finished with their
+  // stores acknowledged; one system-scope release orders both before the flags.
   __threadfence_system();
+  if (lane < s.n_nb && e > 1) store_sys(s.nb_flags[lane] + freed + s.my_rank, e - 1);
   if (lane < s.n_out) store_sys(s.out_flags[lane] + PutFlags::ARRIVED + s.my_rank, e);
-  if (lane < s.n_in) wait_geq(s.my_flags + PutFlags::ARRIVED + s.in_rank[lane], e, s, 0x200 + lane);
+  if (lane < s.n_in && !wait_geq(s.my_flags + PutFlags::ARRIVED + s.in_rank[lane], e, s, 0x200 + lane)) ok = 0;
+  __syncthreads();
+  (void)ok;
+  if (lane == 0) store_sys(s.my_flags + PutFlags::EPOCH, e);  // exchange e complete (unpack reads parity e)
 }
 
 }  // namespace
