@@ -177,7 +177,22 @@ void BufferPool::free_all() {
 
 // ---------------------------------------------------------------- HaloEngine
 
-HaloEngine::HaloEngine(const GridInfo& g) : grid_(g) {}
+HaloEngine::HaloEngine(const GridInfo& g) : grid_(g) {
+  const char* e = std::getenv("IGG_DEBUG_SYNC");
+  debug_sync_ = e && *e && *e != '0';
+}
+
+void HaloEngine::debug_phase(hipStream_t stream, bool device, const char* phase) const {
+  if (!debug_sync_ || !device) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  IGG_HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+  if (cs != hipStreamCaptureStatusNone) return;
+  const hipError_t e = hipStreamSynchronize(stream);
+  const hipError_t l = hipGetLastError();
+  if (e != hipSuccess || l != hipSuccess)
+    fail("IGG_DEBUG_SYNC: update_halo phase '", phase, "' failed: ",
+         hipGetErrorString(e != hipSuccess ? e : l));
+}
 
 HaloEngine::~HaloEngine() {
   if (done_) (void)hipEventDestroy(done_);
@@ -314,13 +329,16 @@ void HaloEngine::exchange_dim_impl(const std::vector<Field>& fields, int dim, bo
   {
     TraceRange r(kPack[dim]);
     do_copies(pack);
+    debug_phase(stream, device, kPack[dim]);
   }
   {
     TraceRange r(kComm[dim]);
     transport_->exchange(recvs, sends, device, stream);
+    debug_phase(stream, device, kComm[dim]);
   }
   TraceRange r(kUnpack[dim]);
   do_copies(unpack);
+  debug_phase(stream, device, kUnpack[dim]);
 }
 
 }  // namespace igg
@@ -479,20 +497,19 @@ void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stre
   {
     TraceRange r("igg.put.pack");
     launch_copy2d(put, eb, stream, /*system_fence=*/true, ParityShift{epoch, half, 1, 1});
+    debug_phase(stream, true, "igg.put.pack");
   }
   {
     TraceRange r("igg.put.sync");
     launch_put_sync(ps, stream);
+    debug_phase(stream, true, "igg.put.sync");
   }
   {
     TraceRange r("igg.put.unpack");
     launch_copy2d(unpack, eb, stream, false, ParityShift{epoch, half, 2, 0});
+    debug_phase(stream, true, "igg.put.unpack");
   }
-  static const bool debug = std::getenv("IGG_PUT_DEBUG") != nullptr;
-  if (debug) {
-    IGG_HIP_CHECK(hipStreamSynchronize(stream));
-    mesh.check_error();
-  }
+  if (debug_sync_) mesh.check_error();  // a bounded wait of this exchange timed out
 }
 
 void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device,
@@ -577,6 +594,7 @@ void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device
   {
     TraceRange r("igg.onephase.pack");
     do_copies(pack);
+    debug_phase(stream, device, "igg.onephase.pack");
   }
   // 2. one communication phase for all remote messages
   std::vector<Copy2D> unpack;
@@ -597,10 +615,12 @@ void HaloEngine::exchange_onephase(const std::vector<Field>& fields, bool device
   if (!tsend.empty() || !trecv.empty()) {
     TraceRange r("igg.onephase.transport");
     tr->exchange(trecv, tsend, device, stream);
+    debug_phase(stream, device, "igg.onephase.transport");
   }
   // 3. unpack every receive region (disjoint: one launch)
   TraceRange r3("igg.onephase.unpack");
   do_copies(unpack);
+  debug_phase(stream, device, "igg.onephase.unpack");
 }
 
 }  // namespace igg

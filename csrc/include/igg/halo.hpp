@@ -164,6 +164,9 @@ class HaloEngine {
   hipEvent_t done_ = nullptr;
   hipStream_t last_stream_ = nullptr;
   bool have_event_ = false;
+  // IGG_DEBUG_SYNC: drain and check the stream after every phase, naming it.
+  void debug_phase(hipStream_t stream, bool device, const char* phase) const;
+  bool debug_sync_ = false;
   // Put transport bookkeeping: exchanges issued, senders of the previous one.
   uint64_t put_count_ = 0;
   std::vector<int> prev_in_;

@@ -101,6 +101,7 @@ class Communicator:
     rccl: object = None
     torch_nccl: object = None
     mesh: object = None  # native.PeerMesh of the 'put' transport
+    _stage: dict = field(default_factory=dict)  # pinned host staging buffers
     local_rank: int = 0
     local_size: int = 1
     _transports: dict = field(default_factory=dict)
@@ -199,15 +200,25 @@ class Communicator:
         for r in reqs:
             r.wait()
 
+    def _pinned(self, role: str, k: int, n: int) -> torch.Tensor:
+        """Grow-only page-locked host staging buffer (reference: registered host
+        buffers, src/shared.jl:117-129): DMA engines copy it without bouncing."""
+        key = (role, k)
+        b = self._stage.get(key)
+        if b is None or b.numel() < n:
+            b = torch.empty(max(n, 1 << 16), dtype=torch.uint8, pin_memory=True)
+            self._stage[key] = b
+        return b[:n]
+
     def _staged_p2p(self, recvs, sends, device, stream):
         """Host-staged device exchange (the reference's non-GPU-aware MPI path,
         update_halo.jl:437,465): D2H of the send buffers, gloo, H2D."""
         hs = []
-        for p, n, peer, tag in sends:
-            h = torch.empty(n, dtype=torch.uint8)
+        for k, (p, n, peer, tag) in enumerate(sends):
+            h = self._pinned("s", k, n)
             native.memcpy_d2h_stream(h.data_ptr(), p, n, stream)
             hs.append((h, peer, tag))
-        hr = [(torch.empty(n, dtype=torch.uint8), p, peer, tag) for p, n, peer, tag in recvs]
+        hr = [(self._pinned("r", k, n), p, peer, tag) for k, (p, n, peer, tag) in enumerate(recvs)]
         reqs = [dist.irecv(h, src=self.global_rank(peer), group=self.gloo, tag=tag) for h, _p, peer, tag in hr]
         reqs += [dist.isend(h, dst=self.global_rank(peer), group=self.gloo, tag=tag) for h, peer, tag in hs]
         for r in reqs:

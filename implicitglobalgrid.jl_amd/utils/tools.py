@@ -1,9 +1,9 @@
 """Global sizes, global coordinates and timing (reference: src/tools.jl).
 
 ``x_g(ix, dx, A)`` keeps the reference's 1-based ``ix`` (so the reference
-doctests and test vectors carry over verbatim); ``x_g_vec`` returns all
-coordinates of an axis as a tensor (0-based vectorised form, used to build
-initial conditions on the device without a host loop).
+doctests and test vectors carry over verbatim); ``coords_g`` returns all
+coordinates of an axis as a tensor (vectorised, same fp64 operation order as
+``x_g`` so both agree bitwise; used to build initial conditions on the device).
 """
 from __future__ import annotations
 
@@ -64,9 +64,18 @@ def z_g(iz: int, dz: float, A) -> float:
 
 def coords_g(dim0: int, d: float, A, *, dtype=torch.float64, device=None) -> torch.Tensor:
     """All global coordinates of axis ``dim0`` (0-based) of ``A`` as a 1-D tensor."""
-    n = _size(A, dim0)
-    v = torch.tensor([_coord(i + 1, d, A, dim0) for i in range(n)], dtype=torch.float64)
-    return v.to(dtype=dtype, device=device if device is not None else A.device)
+    gg = _grid.global_grid()
+    m = _size(A, dim0)
+    n = int(gg.nxyz[dim0])
+    x0 = 0.5 * (n - m) * d
+    base = int(gg.coords[dim0]) * (n - int(gg.overlaps[dim0]))
+    x = (torch.arange(m, dtype=torch.float64) + float(base)) * d + x0  # (base + i - 1) * d + x0, i 1-based
+    if bool(gg.periods[dim0]):
+        ng = int(gg.nxyz_g[dim0])
+        x = x - d
+        x = torch.where(x > (ng - 1) * d, x - ng * d, x)
+        x = torch.where(x < 0, x + ng * d, x)
+    return x.to(dtype=dtype, device=device if device is not None else A.device)
 
 
 # --- timing (tools.jl:205-236) -------------------------------------------------

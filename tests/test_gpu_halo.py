@@ -258,3 +258,24 @@ def test_gpu_loopback_put_transport(gpu, monkeypatch):
     mesh.check_error()
     assert mesh.epoch >= 3 + 3 * 7
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.parametrize("transport", ["rccl", "put"])
+def test_gpu_debug_sync_phases(gpu, monkeypatch, transport):
+    """IGG_DEBUG_SYNC=1 drains and checks the stream after every phase of
+    every schedule; results stay bitwise."""
+    from igg.parallel import halo as H
+
+    monkeypatch.setenv("IGG_DEBUG_SYNC", "1")
+    monkeypatch.setenv("IGG_TRANSPORT", transport)
+    n = (9, 8, 10)
+    igg.init_global_grid(*n, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    H.enable_loopback()
+    for mode in (["sequential", "onephase"] if transport == "rccl" else ["auto"]):
+        H.set_halo_mode(mode)
+        A = encode(torch.zeros(*n, dtype=torch.float32))
+        ref = A.clone()
+        Ag = zero_boundaries(A.clone()).to(gpu)
+        igg.update_halo_(Ag)
+        assert torch.equal(Ag.cpu(), ref)
+    igg.finalize_global_grid(finalize_MPI=False)

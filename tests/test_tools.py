@@ -1,6 +1,7 @@
 """Port of test/test_tools.jl (exact vectors) and the x_g doctests
 (src/tools.jl:66-96), plus tic/toc."""
 import numpy as np
+import pytest
 import torch
 
 import igg
@@ -129,4 +130,18 @@ def test_tic_toc():
     assert isinstance(t0, float)
     t = igg.toc()
     assert isinstance(t, float) and 0 <= t < 5
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.parametrize("per", [0, 1])
+def test_coords_g_vectorised_matches_x_g_bitwise(per):
+    from igg.utils.tools import coords_g, x_g, y_g, z_g
+
+    igg.init_global_grid(13, 9, 7, periodx=per, periody=per, periodz=per, quiet=True, init_MPI=False)
+    for shape in [(13, 9, 7), (14, 9, 7), (12, 10, 8)]:
+        A = torch.empty(shape, device="meta")
+        for dim, f in ((0, x_g), (1, y_g), (2, z_g)):
+            v = coords_g(dim, 0.37, A, device="cpu")
+            ref = torch.tensor([f(i + 1, 0.37, A) for i in range(shape[dim])], dtype=torch.float64)
+            assert torch.equal(v, ref)
     igg.finalize_global_grid(finalize_MPI=False)

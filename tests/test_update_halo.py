@@ -331,3 +331,18 @@ def test_plan_summary_reports_zero_copy():
     assert s[0]["faces"] and all(f["zero_copy"] for f in s[0]["faces"])  # x-faces of C-order arrays
     assert s[1]["faces"] == [] and s[2]["faces"] == []
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_debug_sync_mode_runs(monkeypatch):
+    """IGG_DEBUG_SYNC=1: the engine drains/checks after every phase (host path
+    here: a no-op on CPU fields, but the flag is parsed and the update exact)."""
+    monkeypatch.setenv("IGG_DEBUG_SYNC", "1")
+    igg.init_global_grid(5, 4, 3, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    from tests.helpers import encode, zero_boundaries
+
+    A = encode(torch.zeros(5, 4, 3, dtype=torch.float64))
+    ref = A.clone()
+    X = zero_boundaries(A.clone())
+    igg.update_halo_(X)
+    assert torch.equal(X, ref)
+    igg.finalize_global_grid(finalize_MPI=False)
