@@ -55,6 +55,8 @@ def parse():
                     help="local grid points per dimension (default: per config)")
     ap.add_argument("--dtype", default=None, choices=["float64", "float32"])
     ap.add_argument("--gather-every", type=int, default=None, help="gather_ the field to rank 0 every K steps")
+    ap.add_argument("--gather-mode", default="async", choices=["async", "sync"],
+                    help="async: snapshot + gather_async_ (root pulls with copy engines while stepping continues)")
     ap.add_argument("--overlap", action="store_true", help="boundary/interior split with the halo on a second stream")
     ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
     ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
@@ -163,7 +165,8 @@ def main():
     field = (lambda: model.P) if is2d else (lambda: model.T)
     A_global = None
     if gather_every > 0 and me == 0:
-        A_global = torch.empty([int(v) for v in igg.get_global_grid().nxyz_g][: 2 if is2d else 3],
+        # gather_ concatenates the local blocks (halos included) in Cartesian order
+        A_global = torch.empty([int(d) * int(s) for d, s in zip(dims, field().shape)],
                                dtype=dtype, device=field().device)
     ab = None
     if nprocs > 1 and args.transport == "auto":
@@ -183,13 +186,22 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if gather_every > 0:
-        done = 0
+        done, pending = 0, None
+        snap = torch.empty_like(field()) if args.gather_mode == "async" else None
         while done < args.steps:
             k = min(gather_every, args.steps - done)
             model.run(k)
             done += k
             if done % gather_every == 0:
-                igg.gather_(field(), A_global)
+                if snap is None:
+                    igg.gather_(field(), A_global)
+                else:
+                    if pending is not None:
+                        pending.wait()
+                    snap.copy_(field())
+                    pending = igg.gather_async_(snap, A_global)
+        if pending is not None:
+            pending.wait()
     else:
         model.run(args.steps)
     torch.cuda.synchronize()
@@ -244,6 +256,7 @@ def main():
                 "overlap_comm": bool(getattr(model, "overlap", False)),
                 "gather_every": gather_every,
                 "gather_ms": gather_ms,
+                "gather_mode": args.gather_mode if gather_every > 0 else None,
                 "phase_ms": phase_ms,
                 "t_eff_per_gpu_GBs": round(per_gpu, 3),
                 "a_eff_bytes_per_gpu": model.a_eff_bytes,

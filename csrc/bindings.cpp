@@ -384,6 +384,26 @@ PYBIND11_MODULE(_igg_native, m) {
            })
       .def("free", &Gatherer::free)
       .def_property_readonly("capacity", &Gatherer::capacity);
+  py::class_<PullGatherer>(m, "PullGatherer")
+      .def(py::init([](int rank, int nranks, py::function allgather) {
+             PullGatherer::AllGather ag = [allgather](const std::string& mine) {
+               py::gil_scoped_acquire gil;
+               py::list out = allgather(py::bytes(mine));
+               std::vector<std::string> v;
+               for (auto h : out) v.push_back(h.cast<std::string>());
+               return v;
+             };
+             return std::make_unique<PullGatherer>(rank, nranks, ag);
+           }),
+           py::arg("rank"), py::arg("nranks"), py::arg("allgather"))
+      .def("start", [](PullGatherer& g, const FieldTuple& a, int root, const Int3& dims) {
+        g.start(to_field(a), root, dims);
+      })
+      .def("wait", [](PullGatherer& g, uintptr_t dst, uintptr_t s) {
+        g.wait(reinterpret_cast<void*>(dst), as_stream(s));
+      })
+      .def_property_readonly("pending", &PullGatherer::pending)
+      .def("free", &PullGatherer::free);
   m.def("gather_reorder", [](uintptr_t src, uintptr_t dst, const Int3& s, const Int3& dims,
                              int eb, uintptr_t stream) {
     launch_gather_reorder(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), s, dims,

@@ -9,6 +9,10 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
+#include <string>
+#include <utility>
+#include <vector>
 
 #include <hip/hip_runtime_api.h>
 
@@ -36,6 +40,42 @@ class Gatherer {
  private:
   char* buf_ = nullptr;
   size_t bytes_ = 0;
+};
+
+// Non-blocking gather by root pull (MI355X copy engines). start(): every rank
+// drains its stream (so `a` is final), publishes the IPC handle + offset of the
+// allocation holding `a`; the root enqueues one hipMemcpyAsync per peer
+// (peer -> root staging buffer: a P2P copy over xGMI executed by the SDMA
+// engines, no compute units) plus its own block on a private stream, and
+// returns immediately: the application keeps computing while the data moves.
+// wait(): the root orders the caller's stream after the pulls and reorders
+// into the global layout; every rank then passes a barrier, after which the
+// peers may modify `a` again (MPI_Igather semantics: `a` is read-only until
+// wait() returns). Peer mappings live from start() to wait() only.
+class PullGatherer {
+ public:
+  using AllGather = std::function<std::vector<std::string>(const std::string&)>;
+  PullGatherer(int rank, int nranks, AllGather allgather);
+  ~PullGatherer();
+  PullGatherer(const PullGatherer&) = delete;
+  PullGatherer& operator=(const PullGatherer&) = delete;
+  void start(const Field& a, int root, const Int3& dims);
+  void wait(void* dst, hipStream_t stream);
+  bool pending() const { return pending_; }
+  void free();
+
+ private:
+  int rank_, nranks_;
+  AllGather allgather_;
+  hipStream_t side_ = nullptr;
+  hipEvent_t done_ = nullptr;
+  char* buf_ = nullptr;
+  size_t bytes_ = 0;
+  bool pending_ = false;
+  int root_ = 0;
+  Field field_{};
+  Int3 dims_{1, 1, 1};
+  std::vector<std::pair<std::string, void*>> opened_;  // peer mappings of the pending gather
 };
 
 }  // namespace igg

@@ -23,14 +23,20 @@ from .halo import field_tuple
 
 _host_buf = None  # grow-only flat uint8 host buffer
 _gatherer = None  # native device gatherer (grow-only device buffer)
+_puller = None  # native PullGatherer (gather_async_)
 
 
 def free_gather_buffer() -> None:
-    global _host_buf, _gatherer
+    global _host_buf, _gatherer, _puller
     _host_buf = None
     if _gatherer is not None:
         _gatherer.free()
     _gatherer = None
+    if _puller is not None:
+        if _puller.pending:
+            raise IGGError("free_gather_buffer: a gather_async_ is still pending (call wait() first).")
+        _puller.free()
+    _puller = None
 
 
 def _padded_shape(A: torch.Tensor) -> list[int]:
@@ -111,6 +117,58 @@ def _gather_host(A, A_global, root, s, dims, me, nprocs, c) -> None:
         _global_view(A_global, s, dims).copy_(glob)
     else:
         A_global.copy_(glob.reshape(A_global.shape).to(A_global.device))
+
+
+class GatherHandle:
+    """Result of ``gather_async_``; ``wait()`` completes the gather (collective)."""
+
+    def __init__(self, A_global, done: bool):
+        self._A_global = A_global
+        self._done = done
+
+    def wait(self) -> None:
+        if self._done:
+            return
+        dst = self._A_global
+        _puller.wait(dst.data_ptr() if dst is not None else 0, torch.cuda.current_stream().cuda_stream)
+        self._done = True
+
+    @property
+    def done(self) -> bool:
+        return self._done
+
+
+def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) -> GatherHandle:
+    """Non-blocking ``gather_``: returns a handle whose ``wait()`` (collective)
+    completes it. GPU fields on several ranks: the root pulls every block with
+    the copy engines (peer-to-peer hipMemcpyAsync over xGMI, no compute units)
+    while the application continues; ``A`` must not be modified before
+    ``wait()`` (MPI_Igather semantics) and ``A_global`` (root) must be a
+    C-contiguous GPU tensor. Other cases complete synchronously."""
+    global _puller
+    gg = _grid.global_grid()
+    nprocs, me = int(gg.nprocs), int(gg.me)
+    if not (A.is_cuda and nprocs > 1):
+        gather_(A, A_global, root=root)
+        return GatherHandle(A_global, True)
+    if me == root:
+        if A_global is None:
+            raise IGGError("The input argument A_global can't be `nothing` on the root")
+        if A_global.numel() != nprocs * A.numel():
+            raise IGGError("The input argument A_global must be of length nprocs*length(A)")
+        if A_global.dtype != A.dtype:
+            raise IGGError("The input arguments A and A_global must have the same element type.")
+        if not (A_global.is_cuda and A_global.is_contiguous()):
+            raise IGGError("gather_async_: A_global must be a C-contiguous GPU tensor on the root.")
+        _global_view(A_global, _padded_shape(A), [int(d) for d in gg.dims])
+    if not A.is_contiguous():
+        raise IGGError("gather_async_: A must be contiguous (it is read in place by the root).")
+    if _puller is None:
+        c = gg.comm
+        _puller = native.PullGatherer(me, nprocs, lambda b: c.all_gather_object(bytes(b)))
+    dims = [int(d) for d in gg.dims]
+    _puller.start(field_tuple(A), root, dims)
+    return GatherHandle(A_global if me == root else None, False)
 
 
 gather = gather_

@@ -163,6 +163,35 @@ def scenario_acoustic(dev, nx, ny, steps):
     print(f"rank {me} acoustic OK dims={dims.tolist()}")
 
 
+def scenario_gather_async():
+    """gather_async_: root pulls every block (IPC + copy engine), the caller
+    overlaps other work, wait() reorders; then A may change again."""
+    me, dims, nprocs, coords, comm = igg.init_global_grid(6, 5, 4, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    s = (6, 5, 4)
+    for root in sorted({0, nprocs - 1}):
+        for dt in (torch.float64, torch.float32):
+            A = (torch.full(s, float(me + 1), dtype=torch.float64) * 1000
+                 + torch.arange(120, dtype=torch.float64).view(s)).to(dt).cuda()
+            G = torch.zeros(dims[0] * 6, dims[1] * 5, dims[2] * 4, dtype=dt, device="cuda") if me == root else None
+            h = igg.gather_async_(A, G, root=root)
+            busy = torch.rand(256, 256, device="cuda") @ torch.rand(256, 256, device="cuda")  # overlapped work
+            h.wait()
+            A.fill_(-1)  # allowed after wait()
+            torch.cuda.synchronize()
+            del busy
+            if me == root:
+                Gc = G.cpu().double()
+                for p in range(nprocs):
+                    c = igg.native.cart_coords(p, dims.tolist())
+                    blk = Gc[c[0] * 6:(c[0] + 1) * 6, c[1] * 5:(c[1] + 1) * 5, c[2] * 4:(c[2] + 1) * 4]
+                    exp = (torch.full(s, float(p + 1), dtype=torch.float64) * 1000
+                           + torch.arange(120, dtype=torch.float64).view(s)).to(dt).double()
+                    assert torch.equal(blk, exp), f"root {root}: block of rank {p} wrong"
+    igg.finalize_global_grid()
+    print(f"rank {me} gather_async OK")
+
+
 def scenario_put_timeout():
     """Rank 1 skips one update_halo_: rank 0's bounded waits expire (short
     IGG_PUT_TIMEOUT), its kernels exit, and check_transport reports it."""

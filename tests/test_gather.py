@@ -58,3 +58,15 @@ def test_dtype_mismatch_error():
     with pytest.raises(IGGError):
         igg.gather_(torch.zeros(nx, ny, nz), torch.zeros(nx, ny, nz, dtype=torch.float64))
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_gather_async_single_process_completes():
+    """One process (or host tensors): gather_async_ completes synchronously."""
+    igg.init_global_grid(4, 3, 2, quiet=True, init_MPI=False)
+    A = torch.arange(24, dtype=torch.float64).view(4, 3, 2)
+    G = torch.zeros(4, 3, 2, dtype=torch.float64)
+    h = igg.gather_async_(A, G)
+    assert h.done
+    h.wait()
+    assert torch.equal(G, A)
+    igg.finalize_global_grid(finalize_MPI=False)

@@ -99,3 +99,9 @@ def test_put_transport_timeout_reports_and_never_hangs():
 @pytest.mark.gpu
 def test_put_transport_absorbs_rank_skew():
     run_ranks(4, "put_skew", 12, env_extra=PUT_ENV, timeout=200)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs", [2, 4])
+def test_gather_async_gpu(nprocs):
+    run_ranks(nprocs, "gather_async", env_extra=PUT_ENV)
