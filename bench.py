@@ -57,7 +57,8 @@ def parse():
     ap.add_argument("--gather-every", type=int, default=None, help="gather_ the field to rank 0 every K steps")
     ap.add_argument("--gather-mode", default="async", choices=["async", "sync"],
                     help="async: snapshot + gather_async_ (root pulls with copy engines while stepping continues)")
-    ap.add_argument("--overlap", action="store_true", help="boundary/interior split with the halo on a second stream")
+    ap.add_argument("--overlap", action="store_true",
+                    help="force the boundary/interior split with the halo on a second stream (default: A/B decides)")
     ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
     ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
     ap.add_argument("--loopback", action="store_true",
@@ -116,16 +117,27 @@ def select_transport(model, field, comm, log, ref: str = "rccl") -> tuple[str, d
     bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
     del A, B
     times = {}
-    cands = [ref] + (["put"] if bad == 0.0 else [])
-    for t in cands:
+    cands = [(ref, False)] + ([("put", False)] if bad == 0.0 else [])
+    # Overlap (boundary planes first, exchange on a second stream next to the
+    # interior) only pays without z-neighbours: x/y boundary planes are cheap
+    # rows, z-planes of a C-ordered field are maximally strided. RCCL's p2p
+    # kernels stall next to a full-GPU stencil, so only put is tried overlapped.
+    if bad == 0.0 and getattr(model, "can_overlap", False) and not any(model.sides[2]):
+        cands.append(("put", True))
+    for t, ov in cands:
         H.set_transport(t)
+        if hasattr(model, "set_overlap"):
+            model.set_overlap(ov)
         model.step()
-        times[t] = _timed(model, comm, 10)
-    best = min(times, key=times.get)
-    H.set_transport(best)
-    log(f"transport A/B (ms/step): {', '.join(f'{k}={v * 1e3:.4f}' for k, v in times.items())}"
+        times[f"{t}{'+overlap' if ov else ''}"] = (_timed(model, comm, 10), t, ov)
+    best = min(times, key=lambda k: times[k][0])
+    _, t, ov = times[best]
+    H.set_transport(t)
+    if hasattr(model, "set_overlap"):
+        model.set_overlap(ov)
+    log(f"schedule A/B (ms/step): {', '.join(f'{k}={v[0] * 1e3:.4f}' for k, v in times.items())}"
         f"{'' if bad == 0.0 else ' (put mismatched rccl: excluded)'} -> {best}")
-    return best, {k: round(v * 1e3, 5) for k, v in times.items()}
+    return best, {k: round(v[0] * 1e3, 5) for k, v in times.items()}
 
 
 def main():
@@ -169,7 +181,7 @@ def main():
         A_global = torch.empty([int(d) * int(s) for d, s in zip(dims, field().shape)],
                                dtype=dtype, device=field().device)
     ab = None
-    if nprocs > 1 and args.transport == "auto":
+    if nprocs > 1 and args.transport == "auto" and not args.overlap:
         _, ab = select_transport(model, field(), comm, log, ref="staged" if args.share_gpu else "rccl")
     for _ in range(args.warmup):
         model.step()

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--dtype", default="float64")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--loopback-dims", default="111", help="dims with loopback neighbours, e.g. 110 = x,y only")
     ap.add_argument("--combos", default="0:11:0:0,0:11:0:8,0:11:0:16,0:11:0:32,0:0:0:16",
                     help="interior_rounds:halo_variant:halo_rounds:reserved_cus list")
     a = ap.parse_args()
@@ -53,7 +54,7 @@ def main():
     plain = [timeit(m.step, a.reps, s) for _ in range(a.rounds)]
     del m
     torch.cuda.empty_cache()
-    H.enable_loopback()
+    H.enable_loopback(tuple(c == "1" for c in a.loopback_dims))
     ms = Diffusion3D(dtype=dtype, overlap=False)
     combos = [tuple(int(x) for x in c.split(":")) for c in a.combos.split(",")]
     models = {}

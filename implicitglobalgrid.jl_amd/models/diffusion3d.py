@@ -74,10 +74,14 @@ class Diffusion3D:
         if self.device.type == "cuda":
             self.T, self.Cp, self.T2 = _carve([self.T, self.Cp, self.T2], gap=266240)
         sides = [[bool(gg.neighbors[0, d] != -1), bool(gg.neighbors[1, d] != -1)] for d in range(3)]
-        self.overlap = overlap and self.device.type == "cuda" and any(any(s) for s in sides)
+        self.sides = sides
+        self.can_overlap = self.device.type == "cuda" and any(any(sd) for sd in sides)
         self.inner = [stencil.inner_box(shape)]
-        if self.overlap and self.variant is None:
+        z_split = any(sides[2])
+        if overlap and self.can_overlap and z_split and self.variant is None:
             self.variant = 11  # 128-point tiles: z-slabs stay one full tile wide
+        if self.variant is None and self.device.type == "cuda":
+            self.variant = _choose_variant(self)
         if slab_width is None:
             # A slab at every side with a neighbour, just wide enough to hold
             # the plane update_halo sends there (index ol-1 / n-ol) along dims
@@ -85,21 +89,34 @@ class Diffusion3D:
             # whole cache lines per row) it is exactly one kernel tile wide, so
             # both the slab launch and the interior launch run full tiles.
             o = [int(v) for v in gg.overlaps]
-            v = self.variant if self.variant is not None else 0
-            tile = max(1, int(stencil.native.diffusion3d_variant_tile(v)))
+            tile = max(1, int(stencil.native.diffusion3d_variant_tile(self.variant or 0)))
             slab_width = (max(1, o[0] - 1), max(1, o[1] - 1), max(o[2] - 1, tile - 1))
         self.slabs, self.interior = stencil.split_boundary(shape, sides, slab_width)
-        if self.variant is None and self.device.type == "cuda":
-            self.variant = _choose_variant(self)
+        if self.halo_variant is None and not z_split:
+            self.halo_variant = 18  # x/y boundary planes: the one-row scalar kernel is fastest
         self.compute_stream = None
-        if self.overlap:
-            if reserve_cus > 0:
+        self.halo_stream = None
+        self._reserve_cus = reserve_cus
+        self.overlap = False
+        if overlap:
+            self.set_overlap(True)
+
+    def set_overlap(self, flag: bool) -> bool:
+        """Switch between the serial step and the boundary/interior overlapped
+        step (needs a GPU model with at least one neighbour); returns the mode."""
+        flag = bool(flag) and self.can_overlap
+        if flag and self.halo_stream is None:
+            if self._reserve_cus > 0:
                 from ..utils.streams import cu_partition
 
-                self.compute_stream, self.halo_stream = cu_partition(reserve_cus)
+                self.compute_stream, self.halo_stream = cu_partition(self._reserve_cus)
             else:
                 _least, greatest = torch.cuda.Stream.priority_range()
                 self.halo_stream = torch.cuda.Stream(device=self.device, priority=greatest)
+        if flag != self.overlap:
+            self.graph = None  # a captured schedule no longer matches
+        self.overlap = flag
+        return flag
 
     def _kw(self, variant=None, rounds=0):
         return dict(lam=self.lam, dt=self.dt, dx=self.dx, dy=self.dy, dz=self.dz,
