@@ -18,6 +18,11 @@ transport reproduces the RCCL exchange bitwise on this node, times a few steps
 with each (MAX over ranks) during warm-up and keeps the faster; the timed
 steps are replayed from a hipGraph (two steps per replay) unless --no-graph.
 
+``--fused auto`` (default; diffusion3d with neighbours): the stencil kernel
+itself stores its send planes into the neighbours' IPC-mapped arenas over xGMI
+and a 1-wave kernel synchronises (igg/fused.hpp) — checked bitwise against the
+update_halo_ schedule on every rank, then A/B-timed; the faster is kept.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n 512]
                        [--dtype float64] [--overlap] [--variant V|auto]
                        [--transport auto|rccl|put] [--no-graph]
@@ -30,6 +35,7 @@ import os
 import sys
 import time
 
+FUSED_VARIANTS = (0, 9)  # fused-halo kernel tilings tried by the A/B (benchmarks/fused_sweep.py)
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
@@ -68,6 +74,8 @@ def parse():
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "put"],
                     help="device transport of the halo exchange (multi-GPU / loopback)")
+    ap.add_argument("--fused", default="auto", choices=["auto", "on", "off"],
+                    help="fused halo exchange inside the stencil kernel (diffusion3d; auto: bitwise check + A/B)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on device 0, 'staged' instead of RCCL as the A/B reference")
     return ap.parse_args()
@@ -140,6 +148,62 @@ def select_transport(model, field, comm, log, ref: str = "rccl") -> tuple[str, d
     return best, {k: round(v[0] * 1e3, 5) for k, v in times.items()}
 
 
+def select_fused(model, comm, log, mode: str) -> dict | None:
+    """Fused halo exchange (stencil stores the send planes into the neighbours'
+    arenas; igg/fused.hpp) vs the schedule chosen so far: bitwise check of 4
+    steps from the same state on every rank, then A/B timing (MAX over ranks).
+    ``mode``: auto (keep the faster), on (force when it checks out), off."""
+    import torch
+
+    if mode == "off" or not getattr(model, "can_fuse", False):
+        return None
+    T0, T20 = model.T.clone(), model.T2.clone()
+    model.run(4)
+    ref = model.T.clone()
+    model.T.copy_(T0)
+    model.T2.copy_(T20)
+    ok = False
+    try:
+        model.set_fused(True)
+        model.run(4)
+        model.sync_halo()
+        torch.cuda.synchronize()
+        model.check()
+        ok = bool(torch.equal(ref, model.T))
+    except Exception as e:  # e.g. a sync kernel timed out: the fused path does not work here
+        log(f"fused halo exchange failed its check: {type(e).__name__}: {e}"[:300])
+    bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
+    model.T.copy_(T0)
+    model.T2.copy_(T20)
+    del ref, T0, T20
+    if bad != 0.0:
+        model.fused, model._fprimed, model.graph = False, False, None  # T was restored: halos valid
+        log("fused halo exchange mismatched the update_halo_ path on some rank: excluded")
+        return {"fused_ok": False}
+    model.set_fused(False)
+    model.step()
+    t_unf = _timed(model, comm, 10)
+    # Fused kernel candidates: tiling variant x send mode (0 = stores as
+    # computed, 1 = deferred one x step: robust to slow remote acknowledgements).
+    model.set_fused(True)
+    times = {}
+    for v in FUSED_VARIANTS:
+        for fm in (0, 1):
+            model.fused_variant, model.fused_mode = v, fm
+            model.step()
+            times[(v, fm)] = _timed(model, comm, 10)
+    (v, fm), t_fus = min(times.items(), key=lambda kv: kv[1])
+    model.fused_variant, model.fused_mode = v, fm
+    keep = mode == "on" or t_fus < t_unf
+    model.set_fused(keep)
+    log(f"fused A/B (ms/step): update_halo={t_unf * 1e3:.4f}, "
+        + ", ".join(f"fused v{k[0]}/m{k[1]}={t * 1e3:.4f}" for k, t in times.items())
+        + f" -> {f'fused v{v}/m{fm}' if keep else 'update_halo'}")
+    out = {"fused_ok": True, "update_halo": round(t_unf * 1e3, 5)}
+    out.update({f"fused_v{k[0]}_m{k[1]}": round(t * 1e3, 5) for k, t in times.items()})
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,6 +247,9 @@ def main():
     ab = None
     if nprocs > 1 and args.transport == "auto" and not args.overlap:
         _, ab = select_transport(model, field(), comm, log, ref="staged" if args.share_gpu else "rccl")
+    fused_ab = None
+    if not is2d and not args.overlap and (nprocs > 1 or args.loopback or args.periodic):
+        fused_ab = select_fused(model, comm, log, args.fused)
     for _ in range(args.warmup):
         model.step()
     graph_error = None
@@ -205,6 +272,8 @@ def main():
             model.run(k)
             done += k
             if done % gather_every == 0:
+                if getattr(model, "fused", False):
+                    model.sync_halo()  # fused steps leave the halo planes stale
                 if snap is None:
                     igg.gather_(field(), A_global)
                 else:
@@ -221,9 +290,13 @@ def main():
     t1 = time.perf_counter()
     elapsed = _max_over_ranks(comm, t1 - t0)
     H.check_transport()
+    if hasattr(model, "check"):
+        model.check()
     t_it = elapsed / args.steps
     per_gpu = model.a_eff_bytes / t_it / 1e9
     total = per_gpu * nprocs
+    if getattr(model, "fused", False):
+        model.sync_halo()
     finite = bool(torch.isfinite(field()).all().item())
     phase_ms = None
     if not is2d and nprocs > 1 or args.loopback:
@@ -240,6 +313,8 @@ def main():
         torch.cuda.synchronize()
         comm.barrier()
         tg = time.perf_counter()
+        if getattr(model, "fused", False):
+            model.sync_halo()
         igg.gather_(field(), A_global)
         torch.cuda.synchronize()
         gather_ms = round(_max_over_ranks(comm, time.perf_counter() - tg) * 1e3, 3)
@@ -274,6 +349,9 @@ def main():
                 "a_eff_bytes_per_gpu": model.a_eff_bytes,
                 "transport": H.transport_name(),
                 "transport_ab_ms": ab,
+                "fused_halo": bool(getattr(model, "fused", False)),
+                "fused_kernel": ([model.fused_variant, model.fused_mode] if getattr(model, "fused", False) else None),
+                "fused_ab_ms": fused_ab,
                 "stencil_variant": getattr(model, "variant", None),
                 "stencil_variant_ms": getattr(model, "variant_times", None),
                 "finite": finite,

@@ -12,6 +12,7 @@
 #include "igg/acoustic.hpp"
 #include "igg/comm.hpp"
 #include "igg/copy.hpp"
+#include "igg/fused.hpp"
 #include "igg/gather.hpp"
 #include "igg/halo.hpp"
 #include "igg/ipc.hpp"
@@ -459,6 +460,39 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
         py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
         py::arg("stream") = 0, py::arg("rounds") = 0);
+  m.def("diffusion3d_fused_variant_ok", &diffusion3d_fused_variant_ok);
+  py::class_<FusedHalo, std::shared_ptr<FusedHalo>>(m, "FusedHalo")
+      .def(py::init([](std::shared_ptr<PeerMesh> mesh, const Int3& n, int elem_bytes,
+                       const std::array<std::array<int, 2>, 3>& nb) {
+             return std::make_shared<FusedHalo>(mesh, std::array<int64_t, 3>{n[0], n[1], n[2]}, elem_bytes, nb);
+           }),
+           py::arg("mesh"), py::arg("n"), py::arg("elem_bytes"), py::arg("neighbors"))
+      .def("step",
+           [](FusedHalo& f, uintptr_t t2, uintptr_t t, uintptr_t cp, const std::array<double, 3>& rd2,
+              double dtlam, int variant, int64_t step, bool primed, uintptr_t stream, int rounds, int mode) {
+             TraceRange tr("igg.diffusion3d_fused");
+             DiffusionArgs a{t2, t, cp, {0, 0, 0}, {rd2[0], rd2[1], rd2[2]}, dtlam, 0, rounds};
+             f.step_shape(a);
+             f.step(a, variant, mode, step, primed, as_stream(stream));
+           },
+           py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("rd2"), py::arg("dtlam"), py::arg("variant"),
+           py::arg("step"), py::arg("primed"), py::arg("stream"), py::arg("rounds") = 0, py::arg("mode") = 0)
+      .def("sync", [](FusedHalo& f, uintptr_t s) { f.sync(as_stream(s)); })
+      .def("io", [](FusedHalo& f, int64_t step, bool primed) {
+        const HaloIOArgs io = f.io(step, primed);
+        py::list in, out;
+        for (int d = 0; d < 3; ++d) {
+          in.append(py::make_tuple(io.in[d][0], io.in[d][1]));
+          out.append(py::make_tuple(io.out[d][0], io.out[d][1]));
+        }
+        return py::make_tuple(in, out, io.zpitch);
+      })
+      .def("region_offset", &FusedHalo::region_offset)
+      .def_property_readonly("half_elems", &FusedHalo::half_elems)
+      .def_property_readonly("zpitch", &FusedHalo::zpitch)
+      .def_property_readonly("n_peers", &FusedHalo::n_peers)
+      .def("check_error", [](FusedHalo& f) { f.mesh().check_error(); })
+      .def("close", [](FusedHalo& f) { f.mesh().close(); });
   m.def("split_boundary", [](const Int3& n, const std::array<std::array<bool, 2>, 3>& active,
                              const Int3& w) {
     std::vector<Box> slabs;

@@ -1,0 +1,81 @@
+#include "igg/fused.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace igg {
+
+FusedHalo::FusedHalo(std::shared_ptr<PeerMesh> mesh, const std::array<int64_t, 3>& n, int elem_bytes,
+                     const std::array<std::array<int, 2>, 3>& nb)
+    : mesh_(std::move(mesh)), n_(n), elem_(elem_bytes), nb_(nb) {
+  if (!mesh_) fail("FusedHalo: no peer mesh");
+  if (elem_bytes != 4 && elem_bytes != 8) fail("FusedHalo: only float32/float64 fields");
+  for (int d = 0; d < 3; ++d)
+    if (n[d] < 3) fail("FusedHalo: every local extent must be >= 3");
+  // Region sizes (elements): dim-0 faces [n1][n2], dim-1 [n0][n2], dim-2
+  // [n0][zp] with zp >= n1-2 rounded to 16 (vector stores of up to 16 rows).
+  zp_ = round_up(n[1] - 2, 16);
+  const int64_t sz[3] = {n[1] * n[2], n[0] * n[2], n[0] * zp_};
+  const int64_t g = static_cast<int64_t>(DEVICE_ALIGN) / elem_bytes;
+  int64_t pos = 0;
+  for (int d = 0; d < 3; ++d)
+    for (int s = 0; s < 2; ++s) {
+      off_[d][s] = pos;
+      pos += round_up(sz[d], g);
+    }
+  half_ = pos;
+  mesh_->ensure_arena(static_cast<size_t>(2 * half_ * elem_bytes));  // collective
+
+  // Sync kernel: every distinct neighbour is both a receiver and a sender
+  // (face neighbourhoods are symmetric, periodic or not).
+  std::vector<int> peers;
+  for (int d = 0; d < 3; ++d)
+    for (int s = 0; s < 2; ++s) {
+      const int r = nb[d][s];
+      if (r == PROC_NULL) continue;
+      if (r < 0 || r >= mesh_->nranks()) fail("FusedHalo: neighbour rank ", r, " outside the mesh");
+      if (std::find(peers.begin(), peers.end(), r) == peers.end()) peers.push_back(r);
+    }
+  if (static_cast<int>(peers.size()) > PUT_MAX_PEERS) fail("FusedHalo: too many peers");
+  sync_.my_flags = mesh_->flags(mesh_->rank());
+  for (size_t i = 0; i < peers.size(); ++i) {
+    sync_.out_flags[i] = mesh_->flags(peers[i]);
+    sync_.nb_flags[i] = mesh_->flags(peers[i]);
+    sync_.out_rank[i] = peers[i];
+    sync_.in_rank[i] = peers[i];
+  }
+  sync_.n_out = sync_.n_in = sync_.n_nb = static_cast<int>(peers.size());
+  sync_.my_rank = mesh_->rank();
+  sync_.nranks = mesh_->nranks();
+  sync_.timeout_ticks = mesh_->timeout_ticks();
+}
+
+HaloIOArgs FusedHalo::io(int64_t step, bool primed) const {
+  HaloIOArgs io{};
+  const int64_t eb = elem_;
+  const int64_t wh = (step & 1) * half_, rh = ((step + 1) & 1) * half_;
+  char* mine = mesh_->arena(mesh_->rank());
+  for (int d = 0; d < 3; ++d)
+    for (int s = 0; s < 2; ++s) {
+      const int r = nb_[d][s];
+      if (r == PROC_NULL) continue;
+      // My plane next to side s is the halo at side 1-s of that neighbour.
+      io.out[d][s] = reinterpret_cast<uintptr_t>(mesh_->arena(r) + (wh + off_[d][1 - s]) * eb);
+      if (primed) io.in[d][s] = reinterpret_cast<uintptr_t>(mine + (rh + off_[d][s]) * eb);
+    }
+  io.zpitch = zp_;
+  return io;
+}
+
+void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed,
+                     hipStream_t stream) {
+  for (int d = 0; d < 3; ++d)
+    if (a.n[d] != n_[d]) fail("FusedHalo.step: field shape does not match the fused halo's local grid");
+  if (a.elem_bytes != elem_) fail("FusedHalo.step: field dtype does not match the fused halo");
+  launch_diffusion3d_fused(a, io(step, primed), variant, mode, stream);
+  sync(stream);
+}
+
+void FusedHalo::sync(hipStream_t stream) const { launch_put_sync(sync_, stream); }
+
+}  // namespace igg

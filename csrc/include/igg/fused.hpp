@@ -1,0 +1,71 @@
+// Fused halo exchange of the 3-D diffusion model: the stencil kernel is the
+// pack kernel and the transport.
+//
+// The reference exchanges halos after the compute (update_halo!, pack ->
+// Isend/Irecv -> unpack per dimension, src/update_halo.jl:32-78); on one node
+// of MI355X every GPU can store straight into a neighbour's HBM over xGMI. So
+// a fused step is two launches on one stream:
+//   1. the stencil (launch_diffusion3d_fused): while sweeping the interior it
+//      stores the planes each neighbour needs (x=1/n0-2, y=1/n1-2, z=1/n2-2)
+//      into that neighbour's IPC-mapped, uncached arena, and reads its own
+//      face halos from its arena instead of from the field;
+//   2. the put-transport sync kernel (1 wave): publish "my step arrived" at
+//      every neighbour, wait for theirs (bounded spins, error flag on timeout).
+// The arena has two halves: step i writes half i&1 and reads half (i-1)&1, so
+// a neighbour may run one step ahead without overwriting data still in use;
+// the per-step neighbour barrier of the sync kernel bounds the skew to one.
+// The fields' own halo planes are not touched; sync_halo (update_halo_ of T)
+// materialises them when a caller needs them (gather, output, mode switch).
+// Results are bitwise identical to stencil + update_halo_ (tests/test_fused.py).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <memory>
+
+#include <hip/hip_runtime_api.h>
+
+#include "igg/peer.hpp"
+#include "igg/put.hpp"
+#include "igg/stencil.hpp"
+
+namespace igg {
+
+class FusedHalo {
+ public:
+  // nb[d][s]: rank of the neighbour at side s (0 = low, 1 = high) of dim d in
+  // the mesh's numbering, PROC_NULL if none. Collective over the mesh (sizes
+  // the arena; every rank has the same local shape).
+  FusedHalo(std::shared_ptr<PeerMesh> mesh, const std::array<int64_t, 3>& n, int elem_bytes,
+            const std::array<std::array<int, 2>, 3>& nb);
+
+  // Arena regions of the step with counter `step` (writes half step&1; reads
+  // half (step-1)&1 if `primed`, else the field's own halo planes).
+  HaloIOArgs io(int64_t step, bool primed) const;
+  // Stencil with fused send/receive + sync kernel, on `stream`.
+  void step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed, hipStream_t stream);
+  // Fill the shape/dtype of `a` from this halo's local grid.
+  void step_shape(DiffusionArgs& a) const {
+    for (int d = 0; d < 3; ++d) a.n[d] = n_[d];
+    a.elem_bytes = elem_;
+  }
+  // Only the sync kernel (e.g. to rehearse the barrier cost).
+  void sync(hipStream_t stream) const;
+
+  int64_t region_offset(int d, int s) const { return off_[d][s]; }  // elements within a half
+  int64_t half_elems() const { return half_; }
+  int64_t zpitch() const { return zp_; }
+  int n_peers() const { return sync_.n_out; }
+  PeerMesh& mesh() { return *mesh_; }
+
+ private:
+  std::shared_ptr<PeerMesh> mesh_;
+  std::array<int64_t, 3> n_;
+  int elem_;
+  std::array<std::array<int, 2>, 3> nb_;
+  int64_t off_[3][2];
+  int64_t half_ = 0, zp_ = 0;
+  PutSync sync_{};
+};
+
+}  // namespace igg

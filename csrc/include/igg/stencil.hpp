@@ -45,6 +45,23 @@ int diffusion3d_get_rounds();
 
 void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, int variant,
                         hipStream_t stream);
+
+// Fused halo exchange (see fused.hpp): the inner-box update additionally
+// stores its send planes into the receivers' arena regions (`out`, 0 = no
+// receiver at that side) and takes its face halos from its own arena regions
+// (`in`, 0 = read the field's halo planes). Region layouts (elements):
+//   dim 0 faces [n1][n2], dim 1 faces [n0][n2], dim 2 faces [n0][zpitch]
+//   (index x*zpitch + (y-1)). Needs a vector variant (fused_variant_ok) and
+//   n2 % vz == 0.
+struct HaloIOArgs {
+  uintptr_t in[3][2];
+  uintptr_t out[3][2];
+  int64_t zpitch;
+};
+bool diffusion3d_fused_variant_ok(int v);
+// mode 0: sends stored as computed; 1: deferred one x step (see fused_kernels.hip).
+void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
+                              hipStream_t stream);
 void host_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes);
 
 // Boundary-slab / interior decomposition of the inner box [1,n-1)^3.

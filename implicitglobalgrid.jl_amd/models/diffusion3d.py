@@ -16,6 +16,14 @@ MI355X design of a time step (``overlap=True`` and at least one neighbour):
 Both read T only; they write disjoint parts of T2, so the exchange hides behind
 the interior update. Without neighbours (1 GPU, non-periodic) the step is one
 fused kernel and update_halo_ is a no-op, as in the reference.
+
+``fused=True`` (GPU, at least one neighbour; csrc/include/igg/fused.hpp): the
+stencil kernel itself stores the send planes into the neighbours' IPC-mapped
+arenas over xGMI while it sweeps, and reads its face halos from its own arena;
+a 1-wave sync kernel is the whole exchange. The fields' halo planes are then
+stale until ``sync_halo()`` (update_halo_ of T), which ``run``/``capture``
+callers invoke before reading halos (gather, output). Interior values are
+bitwise identical to the update_halo_ path.
 """
 from __future__ import annotations
 
@@ -100,6 +108,61 @@ class Diffusion3D:
         self.overlap = False
         if overlap:
             self.set_overlap(True)
+        # Fused halo exchange (set_fused): native FusedHalo, step counter (arena
+        # half parity), whether the arena holds the halos of the current T.
+        self.fused = False
+        # Fused kernel: variant (tiling; one with a fused instantiation) and
+        # send mode (0 stores as computed, 1 deferred one x step).
+        self.fused_variant = 0
+        self.fused_mode = 0
+        self._fh = None
+        self._fstep = 0
+        self._fprimed = False
+        self._graph_fused = None  # fused mode / step parity the graph was captured with
+        self._graph_parity = 0
+
+    @property
+    def can_fuse(self) -> bool:
+        """Fused halo exchange possible: GPU, a neighbour, overlap 2 where split,
+        n2 a multiple of 4 (vector kernels)."""
+        gg = _grid.global_grid()
+        if self.device.type != "cuda" or not any(any(sd) for sd in self.sides):
+            return False
+        if any(any(self.sides[d]) and int(gg.overlaps[d]) != 2 for d in range(3)):
+            return False
+        return int(self.T.shape[2]) % 4 == 0 and int(self.T.shape[2]) >= 8
+
+    def set_fused(self, flag: bool) -> bool:
+        """Switch the fused halo exchange on/off (collective: every rank at the
+        same point; the first switch-on creates the peer mesh). Switching off
+        materialises the halos first. Returns the mode."""
+        flag = bool(flag) and self.can_fuse
+        if flag == self.fused:
+            return flag
+        if flag:
+            if self._fh is None:
+                self._fh = _make_fused_halo(self)
+            if not stencil.native.diffusion3d_fused_variant_ok(int(self.fused_variant)):
+                self.fused_variant = 0
+            self.set_overlap(False)
+            self._fprimed = False  # the field's halo planes are valid right now
+        else:
+            self.sync_halo()
+        self.fused = flag
+        self.graph = None
+        return flag
+
+    def sync_halo(self) -> None:
+        """Materialise the halo planes of T (fused mode leaves them stale):
+        one update_halo_(T). Later fused steps read halos from T again."""
+        if self.fused and self._fprimed:
+            update_halo_(self.T)
+            self._fprimed = False
+
+    def check(self) -> None:
+        """Raise if a fused-exchange sync kernel timed out waiting for a neighbour."""
+        if self._fh is not None:
+            self._fh.check_error()
 
     def set_overlap(self, flag: bool) -> bool:
         """Switch between the serial step and the boundary/interior overlapped
@@ -125,7 +188,19 @@ class Diffusion3D:
     def step(self) -> None:
         """Advance one time step (T <- T2 after the update and halo exchange)."""
         T, T2, Cp = self.T, self.T2, self.Cp
-        if self.overlap:
+        if self.fused:
+            rd2 = [1.0 / self.dx ** 2, 1.0 / self.dy ** 2, 1.0 / self.dz ** 2]
+            s = torch.cuda.current_stream().cuda_stream
+            if self.timer is not None:
+                with self.timer.phase("stencil+exchange"):
+                    self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
+                                  self.fused_variant, self._fstep, self._fprimed, s, 0, self.fused_mode)
+            else:
+                self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
+                              self.fused_variant, self._fstep, self._fprimed, s, 0, self.fused_mode)
+            self._fstep += 1
+            self._fprimed = True
+        elif self.overlap:
             # 1. boundary slabs on the compute stream (full bandwidth, nothing
             #    else running), 2. the halo exchange of T2 on the high-priority
             #    stream after an event, 3. the interior concurrently on the
@@ -169,6 +244,8 @@ class Diffusion3D:
             raise RuntimeError("Diffusion3D.capture: hipGraphs need a GPU model")
         if not self._warm:
             self.step()
+        if self.fused and not self._fprimed:
+            self.step()  # captured fused steps read the arena: it must hold T's halos
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
@@ -177,12 +254,21 @@ class Diffusion3D:
         torch.cuda.synchronize()
         register_graph(g)
         self.graph = g
+        self._graph_fused = self.fused
+        self._graph_parity = self._fstep % 2
 
     def run(self, nt: int) -> None:
         """Advance ``nt`` steps (by graph replays of two steps if captured)."""
-        if self.graph is not None:
+        if self.graph is not None and self._graph_fused == self.fused:
+            # The captured fused steps have their arena halves baked in: they
+            # assume a primed arena and the step-counter parity of the capture.
+            while self.fused and nt > 0 and (self._fstep % 2 != self._graph_parity or not self._fprimed):
+                self.step()
+                nt -= 1
             for _ in range(nt // 2):
                 self.graph.replay()
+            if self.fused:
+                self._fstep += 2 * (nt // 2)
             nt %= 2
         for _ in range(nt):
             self.step()
@@ -191,6 +277,20 @@ class Diffusion3D:
     def a_eff_bytes(self) -> int:
         """A_eff = (2*D_u + D_k) * n_local * sizeof(T) with D_u = D_k = 1."""
         return 3 * self.T.numel() * self.T.element_size()
+
+
+def _make_fused_halo(m: "Diffusion3D"):
+    """Native FusedHalo over a dedicated peer mesh (collective over the grid)."""
+    from .._native import native
+
+    gg = _grid.global_grid()
+    nb = [[int(gg.neighbors[s, d]) for s in range(2)] for d in range(3)]
+    if gg.nprocs > 1:
+        mesh = native.PeerMesh(gg.comm.rank, gg.comm.size, gg.comm._allgather_bytes)
+    else:  # periodic / loopback single process: every neighbour is this rank
+        nb = [[0 if v >= 0 else -1 for v in row] for row in nb]
+        mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
+    return native.FusedHalo(mesh, list(m.T.shape), m.T.element_size(), nb)
 
 
 def _carve(tensors, gap: int):

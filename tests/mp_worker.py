@@ -129,6 +129,43 @@ def scenario_diffusion(dev, nx, ny, nz, steps, overlap):
     print(f"rank {me} diffusion OK err={err:.2e}")
 
 
+def scenario_diffusion_fused(nx, ny, nz, steps, periodic, graph):
+    """Fused halo exchange (stencil stores send planes into the neighbours'
+    arenas) vs stencil + update_halo_: bitwise equal T on every rank."""
+    from igg.models.diffusion3d import Diffusion3D
+
+    device = _device("gpu")
+    nx, ny, nz, steps, per = int(nx), int(ny), int(nz), int(steps), int(periodic)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, periodx=per, periody=per, periodz=per,
+                                                          quiet=True, select_device=False)
+    v = int(os.environ.get("IGG_TEST_VARIANT", "0"))
+    a = Diffusion3D(dtype=torch.float64, device=device, variant=v)
+    b = Diffusion3D(dtype=torch.float64, device=device, variant=v)
+    b.fused_variant, b.fused_mode = v, int(os.environ.get("IGG_TEST_FUSED_MODE", "0"))
+    assert b.set_fused(True), "fused mode unavailable"
+    a.run(steps)
+    if int(graph):
+        b.step()
+        b.capture()
+        b.run(steps - 1)
+    else:
+        b.run(steps)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    if not torch.equal(a.T, b.T):
+        bad = (a.T != b.T).nonzero()[:5].tolist()
+        raise AssertionError(f"rank {me} dims {dims.tolist()}: fused differs at {bad}")
+    # switching back to the update_halo_ path continues bitwise
+    b.set_fused(False)
+    a.run(3)
+    b.run(3)
+    torch.cuda.synchronize()
+    assert torch.equal(a.T, b.T), f"rank {me}: mismatch after leaving fused mode"
+    igg.finalize_global_grid()
+    print(f"rank {me} fused OK")
+
+
 def scenario_acoustic(dev, nx, ny, steps):
     """2-D staggered acoustic solver on a 2-D process grid vs the same physics
     on the implicit global grid in one array (bitwise on CPU)."""

@@ -1,0 +1,134 @@
+"""Fused halo exchange of the diffusion model (csrc/include/igg/fused.hpp).
+
+The stencil kernel stores its send planes into the neighbours' arenas and reads
+its own face halos from its arena; results must equal stencil + update_halo_
+bitwise (the reference's step, examples/diffusion3D_multigpu_CuArrays_novis.jl:
+42-47). Single process here: periodic grids (every neighbour is this rank) and
+the loopback emulation; multi-rank runs are in test_multiprocess.py.
+"""
+import pytest
+import torch
+
+import igg
+from igg.models.diffusion3d import Diffusion3D
+
+
+def test_fused_unavailable_on_cpu():
+    igg.init_global_grid(12, 10, 16, periodx=1, quiet=True, init_MPI=False, device_type="none")
+    m = Diffusion3D(dtype=torch.float64, device="cpu")
+    assert not m.can_fuse
+    assert m.set_fused(True) is False
+    m.run(2)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_fused_unavailable_without_neighbours(gpu):
+    igg.init_global_grid(12, 10, 16, quiet=True, init_MPI=False)
+    m = Diffusion3D(dtype=torch.float64)
+    assert not m.can_fuse and m.set_fused(True) is False
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+def _pair(n, periods, dtype, variant, loopback=False, mode=0):
+    from igg.parallel import halo as H
+
+    igg.init_global_grid(*n, periodx=periods[0], periody=periods[1], periodz=periods[2], quiet=True,
+                         init_MPI=False)
+    if loopback:
+        H.enable_loopback()
+    a = Diffusion3D(dtype=dtype, variant=variant)
+    b = Diffusion3D(dtype=dtype, variant=variant)
+    b.fused_variant, b.fused_mode = variant, mode
+    assert b.set_fused(True)
+    return a, b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("variant", [0, 2, 9, 11, 14])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_fused_periodic_matches_update_halo(gpu, variant, dtype, mode):
+    a, b = _pair((34, 29, 136), (1, 1, 1), dtype, variant, mode=mode)
+    a.run(9)
+    b.run(9)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("periods", [(1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 0), (0, 1, 1)])
+def test_fused_partial_periodic(gpu, periods):
+    """Only some sides have a neighbour; the others keep their boundary values."""
+    a, b = _pair((21, 19, 64), periods, torch.float64, 11, mode=int(sum(periods) == 1))
+    a.run(6)
+    b.run(6)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_fused_loopback_graph_and_mode_switches(gpu):
+    """Loopback grid, hipGraph replays with odd/even step counts, sync_halo in
+    between (re-primes from the field) and switching back to update_halo_."""
+    a, b = _pair((40, 36, 72), (1, 1, 1), torch.float64, 2, loopback=True, mode=1)
+    a.run(3)
+    b.run(3)
+    b.capture()  # counter odd: the graph bakes in that parity
+    a.run(8)
+    b.run(8)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    assert torch.equal(a.T, b.T)
+    a.run(5)
+    b.run(5)  # unprimed after sync_halo: an eager step first, then replays
+    b.set_fused(False)
+    a.run(2)
+    b.run(2)
+    torch.cuda.synchronize()
+    assert torch.equal(a.T, b.T)
+    assert b.set_fused(True)
+    a.run(4)
+    b.run(4)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_fused_arena_layout(gpu):
+    """Region offsets are 256 B aligned and the z-face pitch covers n1-2 rows."""
+    a, b = _pair((20, 37, 64), (1, 1, 1), torch.float64, 0)
+    fh = b._fh
+    assert fh.zpitch >= 35 and fh.zpitch % 16 == 0
+    for d in range(3):
+        for s in range(2):
+            assert (fh.region_offset(d, s) * 8) % 256 == 0
+    ins, outs, zp = fh.io(0, False)
+    assert all(p == 0 for pair in ins for p in pair)  # unprimed: halos from the field
+    ins, outs, zp = fh.io(1, True)
+    assert all(p != 0 for pair in ins for p in pair) and all(p != 0 for pair in outs for p in pair)
+    assert fh.n_peers == 1
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [(4, 4, 8), (5, 40, 8), (9, 4, 132)])
+def test_fused_tiny_extents(gpu, n):
+    """Tiny extents: the two send planes are neighbours (n=4), a wave holds
+    both y send rows, a single z tile / wave holds both z edges."""
+    for mode in (0, 1):
+        a, b = _pair(n, (1, 1, 1), torch.float64, 0, mode=mode)
+        a.run(5)
+        b.run(5)
+        b.sync_halo()
+        torch.cuda.synchronize()
+        assert torch.equal(a.T, b.T), (n, mode)
+        igg.finalize_global_grid(finalize_MPI=False)

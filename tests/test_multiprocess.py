@@ -105,3 +105,15 @@ def test_put_transport_absorbs_rank_skew():
 @pytest.mark.parametrize("nprocs", [2, 4])
 def test_gather_async_gpu(nprocs):
     run_ranks(nprocs, "gather_async", env_extra=PUT_ENV)
+
+
+# --- fused halo exchange (stencil kernel stores into the neighbours' arenas)
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 0, 0), ("0", "0")),
+                                               (4, (20, 22, 32, 5, 1, 1), ("9", "1")),
+                                               (8, (18, 20, 40, 7, 0, 0), ("0", "1")),
+                                               (8, (16, 18, 24, 6, 1, 1), ("11", "0"))])
+def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
+    # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
+    env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
+    run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=200)
