@@ -35,7 +35,9 @@ import os
 import sys
 import time
 
-FUSED_VARIANTS = (0, 9)  # fused-halo kernel tilings tried by the A/B (benchmarks/fused_sweep.py)
+# Fused-halo kernel candidates of the A/B: (tiling variant, send mode, grid
+# residency rounds) - the front of benchmarks/fused_sweep.py --grid on MI355X.
+FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
@@ -187,20 +189,20 @@ def select_fused(model, comm, log, mode: str) -> dict | None:
     # computed, 1 = deferred one x step: robust to slow remote acknowledgements).
     model.set_fused(True)
     times = {}
-    for v in FUSED_VARIANTS:
-        for fm in (0, 1):
-            model.fused_variant, model.fused_mode = v, fm
-            model.step()
-            times[(v, fm)] = _timed(model, comm, 10)
-    (v, fm), t_fus = min(times.items(), key=lambda kv: kv[1])
-    model.fused_variant, model.fused_mode = v, fm
+    for v, fm, gr in FUSED_CANDIDATES:
+        model.fused_variant, model.fused_mode, model.fused_rounds = v, fm, gr
+        model.step()
+        times[(v, fm, gr)] = _timed(model, comm, 10)
+    best, t_fus = min(times.items(), key=lambda kv: kv[1])
+    model.fused_variant, model.fused_mode, model.fused_rounds = best
     keep = mode == "on" or t_fus < t_unf
     model.set_fused(keep)
+    name = lambda k: f"v{k[0]}/m{k[1]}/r{k[2]}"  # noqa: E731
     log(f"fused A/B (ms/step): update_halo={t_unf * 1e3:.4f}, "
-        + ", ".join(f"fused v{k[0]}/m{k[1]}={t * 1e3:.4f}" for k, t in times.items())
-        + f" -> {f'fused v{v}/m{fm}' if keep else 'update_halo'}")
+        + ", ".join(f"fused {name(k)}={t * 1e3:.4f}" for k, t in times.items())
+        + f" -> {'fused ' + name(best) if keep else 'update_halo'}")
     out = {"fused_ok": True, "update_halo": round(t_unf * 1e3, 5)}
-    out.update({f"fused_v{k[0]}_m{k[1]}": round(t * 1e3, 5) for k, t in times.items()})
+    out.update({f"fused_{name(k)}": round(t * 1e3, 5) for k, t in times.items()})
     return out
 
 
@@ -350,7 +352,9 @@ def main():
                 "transport": H.transport_name(),
                 "transport_ab_ms": ab,
                 "fused_halo": bool(getattr(model, "fused", False)),
-                "fused_kernel": ([model.fused_variant, model.fused_mode] if getattr(model, "fused", False) else None),
+                "fused_kernel": ({"variant": model.fused_variant, "mode": model.fused_mode,
+                                  "grid_rounds": model.fused_rounds} if getattr(model, "fused", False) else None),
+                "stencil_grid_rounds": getattr(model, "rounds", None),
                 "fused_ab_ms": fused_ab,
                 "stencil_variant": getattr(model, "variant", None),
                 "stencil_variant_ms": getattr(model, "variant_times", None),

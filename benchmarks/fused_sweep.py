@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variants", default="0,2,9,11,14")
     ap.add_argument("--dtype", default="float64")
+    ap.add_argument("--grid", action="store_true",
+                    help="grid search: rounds x send mode for fused3/fused6 of each variant")
     a = ap.parse_args()
     n = a.n
     igg.init_global_grid(n, n, n, periodx=1, periody=1, periodz=1, quiet=True)
@@ -63,11 +65,27 @@ def main():
     print("sync kernel alone: %.4f ms" % timed(lambda: fh6.sync(s), a.reps))
     k = [0]
 
-    def fused(fh, v):
+    def fused(fh, v, rounds=0, mode=0):
         def f():
-            fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, 1e-4, v, k[0], True, s)
+            fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, 1e-4, v, k[0], True, s, rounds, mode)
             k[0] += 1
         return f
+
+    if a.grid:
+        for v in (int(x) for x in a.variants.split(",")):
+            for rounds in (1, 2, 3, 4):
+                base = timed(lambda: native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], rd2,
+                                                        1e-4, eb, inner, True, v, s, rounds), a.reps)
+                row = [f"plain {base:.4f}"]
+                for mode in (0, 1):
+                    t0 = timed(fused(fh0, v, rounds, mode), a.reps)
+                    t3 = timed(fused(fh3, v, rounds, mode), a.reps)
+                    t6 = timed(fused(fh6, v, rounds, mode), a.reps)
+                    row.append(f"m{mode}: none {t0:.4f} f3 {t3:.4f} f6 {t6:.4f}")
+                print(f"variant {v:2d} rounds {rounds}: " + " | ".join(row), flush=True)
+        mesh.check_error()
+        igg.finalize_global_grid()
+        return
 
     for v in (int(x) for x in a.variants.split(",")):
         base = timed(lambda: native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], rd2, 1e-4, eb,

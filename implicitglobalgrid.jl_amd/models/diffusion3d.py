@@ -55,6 +55,7 @@ class Diffusion3D:
         self.dz = lz / (nz_g() - 1)
         self.dt = min(self.dx ** 2, self.dy ** 2, self.dz ** 2) * cp_min / lam / 8.1
         self.variant = variant
+        self.rounds = 0  # grid residency rounds of the full-interior launch (0: library default)
         self.variant_times = None  # per-variant ms when autotuned (see _choose_variant)
         self.timer = None  # optional utils.trace.PhaseTimer (eager steps only)
         # Overlap tuning knobs: kernel variant / grid rounds of the boundary
@@ -115,6 +116,7 @@ class Diffusion3D:
         # send mode (0 stores as computed, 1 deferred one x step).
         self.fused_variant = 0
         self.fused_mode = 0
+        self.fused_rounds = 3  # grid residency rounds (profiles/r1_fused/grid.log)
         self._fh = None
         self._fstep = 0
         self._fprimed = False
@@ -181,9 +183,10 @@ class Diffusion3D:
         self.overlap = flag
         return flag
 
-    def _kw(self, variant=None, rounds=0):
+    def _kw(self, variant=None, rounds=None):
         return dict(lam=self.lam, dt=self.dt, dx=self.dx, dy=self.dy, dz=self.dz,
-                    variant=self.variant if variant is None else variant, rounds=rounds)
+                    variant=self.variant if variant is None else variant,
+                    rounds=self.rounds if rounds is None else rounds)
 
     def step(self) -> None:
         """Advance one time step (T <- T2 after the update and halo exchange)."""
@@ -194,10 +197,12 @@ class Diffusion3D:
             if self.timer is not None:
                 with self.timer.phase("stencil+exchange"):
                     self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
-                                  self.fused_variant, self._fstep, self._fprimed, s, 0, self.fused_mode)
+                                  self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
+                                  self.fused_mode)
             else:
                 self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
-                              self.fused_variant, self._fstep, self._fprimed, s, 0, self.fused_mode)
+                              self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
+                              self.fused_mode)
             self._fstep += 1
             self._fprimed = True
         elif self.overlap:
@@ -317,7 +322,8 @@ def _choose_variant(m: "Diffusion3D") -> int:
         return int(env)
     rd2 = [1.0 / m.dx ** 2, 1.0 / m.dy ** 2, 1.0 / m.dz ** 2]
     boxes = [(list(b[0]), list(b[1])) for b in m.inner]
-    t = stencil.time_variants(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes, stencil.SHORTLIST)
+    t = stencil.time_variants(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes,
+                              [(v, r) for v in stencil.SHORTLIST for r in stencil.GRID_ROUNDS])
     cands = sorted(t)
     tot = torch.tensor([t[v] for v in cands], dtype=torch.float64)
     gg = _grid.global_grid()
@@ -325,8 +331,10 @@ def _choose_variant(m: "Diffusion3D") -> int:
         import torch.distributed as dist
 
         dist.all_reduce(tot, group=gg.comm.gloo)
-    m.variant_times = {int(v): round(float(x) / max(1, int(gg.nprocs)), 5) for v, x in zip(cands, tot)}
-    return int(cands[int(torch.argmin(tot))])
+    m.variant_times = {f"{v}@r{r}": round(float(x) / max(1, int(gg.nprocs)), 5) for (v, r), x in zip(cands, tot)}
+    v, r = cands[int(torch.argmin(tot))]
+    m.rounds = int(r)
+    return int(v)
 
 
 def t_eff_gbs(model: Diffusion3D, t_it: float) -> float:

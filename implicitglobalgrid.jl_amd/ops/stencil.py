@@ -58,25 +58,34 @@ def _variant_for(T, boxes, rd2, dtlam, T2, Cp, stream) -> int:
 # Variants that win somewhere on MI355X (sweeps in profiles/): v4_by4_ry4_nt,
 # v2_by4_ry4_pf_nt, v4_by4_ry4, v4_by4_ry8_nt, v2_by4_ry8_nt, v4_bz2_by2_ry8_nt.
 SHORTLIST = (0, 2, 3, 9, 11, 14)
+# Grid residency rounds tried per variant by the model autotune: 1 measured best
+# on some boxes, 3 on others (profiles/r1_fused/grid.log: 1-2.5 %).
+GRID_ROUNDS = (1, 3)
 
 
 def time_variants(T2, T, Cp, rd2, dtlam, boxes, candidates=None, reps: int = 5, rounds: int = 3) -> dict:
-    """Median-of-rounds time (ms) of each candidate variant on these arrays,
-    interleaved (the update is pure: T2 = f(T, Cp), so T2 can be scribbled)."""
+    """Median-of-rounds time (ms) of each candidate on these arrays, interleaved
+    (the update is pure: T2 = f(T, Cp), so T2 can be scribbled). A candidate is
+    a variant index or a (variant, grid_rounds) pair (grid residency rounds of
+    the launch, see diffusion3d_)."""
     n = list(T.shape)
     cands = list(range(len(variants()))) if candidates is None else list(candidates)
     s = torch.cuda.current_stream()
-    times = {v: [] for v in cands}
-    for v in cands:  # warm every code object once
+    times = {c: [] for c in cands}
+
+    def launch(c):
+        v, gr = (c, 0) if isinstance(c, int) else c
         native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(), boxes, True,
-                           v, s.cuda_stream)
+                           v, s.cuda_stream, gr)
+
+    for v in cands:  # warm every code object once
+        launch(v)
     for _ in range(rounds):
         for v in cands:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(reps):
-                native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(),
-                                   boxes, True, v, s.cuda_stream)
+                launch(v)
             e1.record(s)
             e1.synchronize()
             times[v].append(e0.elapsed_time(e1) / reps)
