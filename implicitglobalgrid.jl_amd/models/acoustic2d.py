@@ -23,6 +23,7 @@ from .. import parallel  # noqa: F401
 from .._native import native
 from ..parallel import grid as _grid
 from ..parallel.halo import register_graph, update_halo_
+from .diffusion3d import GRAPH_STEPS
 from ..utils.tools import coords_g, nx_g, ny_g
 
 
@@ -51,6 +52,7 @@ class Acoustic2D:
         self.Vy = torch.zeros((nx, ny + 1), dtype=dtype, device=self.device)
         self.P2, self.Vx2, self.Vy2 = self.P.clone(), self.Vx.clone(), self.Vy.clone()
         self.graph = None
+        self.graph_steps = 2
         self._warm = False
 
     def _update(self, P2, Vx2, Vy2, P, Vx, Vy) -> None:
@@ -68,26 +70,31 @@ class Acoustic2D:
         self.Vy, self.Vy2 = self.Vy2, self.Vy
         self._warm = True
 
-    def capture(self) -> None:
-        """hipGraph of two steps (buffers back in their roles after a replay)."""
+    def capture(self, steps: int = GRAPH_STEPS) -> None:
+        """hipGraph of ``steps`` (even) time steps: buffers are back in their
+        roles after a replay; replay launch overhead (~9 us on MI355X) is paid
+        once per ``steps``."""
         if self.device.type != "cuda":
             raise RuntimeError("Acoustic2D.capture: hipGraphs need a GPU model")
+        if steps < 2 or steps % 2:
+            raise ValueError("Acoustic2D.capture: steps must be even and >= 2")
         if not self._warm:
             self.step()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self.step()
-            self.step()
+            for _ in range(steps):
+                self.step()
         torch.cuda.synchronize()
         register_graph(g)
         self.graph = g
+        self.graph_steps = steps
 
     def run(self, nt: int) -> None:
         if self.graph is not None:
-            for _ in range(nt // 2):
+            for _ in range(nt // self.graph_steps):
                 self.graph.replay()
-            nt %= 2
+            nt %= self.graph_steps
         for _ in range(nt):
             self.step()
 

@@ -38,6 +38,11 @@ from ..parallel.halo import register_graph, update_halo_
 from ..utils.tools import coords_g, nx_g, ny_g, nz_g
 
 
+# Time steps per captured hipGraph (even): one replay launch (~9 us) per
+# GRAPH_STEPS steps instead of per 2 (profiles/r1_fused/graph_gaps.txt).
+GRAPH_STEPS = 10
+
+
 class Diffusion3D:
     def __init__(self, *, dtype=torch.float64, device=None, lam: float = 1.0, cp_min: float = 1.0,
                  lx: float = 10.0, ly: float = 10.0, lz: float = 10.0, overlap: bool = False,
@@ -65,6 +70,7 @@ class Diffusion3D:
         self.halo_rounds = halo_rounds
         self.interior_first = False
         self.graph = None
+        self.graph_steps = 2
         self._warm = False
         shape = (nx, ny, nz)
         probe = torch.empty(shape, device="meta")  # sizes only, for coords_g
@@ -235,16 +241,22 @@ class Diffusion3D:
         self.T, self.T2 = T2, T
         self._warm = True
 
-    def capture(self) -> None:
-        """Record two time steps (T -> T2 -> T) in a hipGraph for ``run``.
+    def capture(self, steps: int = None) -> None:
+        """Record ``steps`` (even, default GRAPH_STEPS) time steps in a hipGraph for ``run``.
 
-        A step is a chain of short launches (stencil, pack, RCCL group, unpack
-        per dimension) whose gaps are host launch latency; replaying a graph
-        removes that latency. Two steps are captured so the ping-pong buffers
-        are back in their roles after every replay. Needs one eager step first
-        (halo buffers, plan cache and kernel variant are set up outside the
-        capture); ``capture`` performs that step itself if none ran yet.
+        A step is a chain of launches (stencil, pack, RCCL group, unpack per
+        dimension; or fused stencil + sync) whose gaps are host launch latency;
+        replaying a graph removes that latency, and a graph replay costs ~9 us
+        to launch on MI355X (profiles/r1_fused/), so several steps are captured
+        per graph. An even count puts the ping-pong buffers back in their roles
+        after every replay. Needs one eager step first (halo buffers, plan
+        cache and kernel variant are set up outside the capture); ``capture``
+        performs that step itself if none ran yet (and one fused step if the
+        fused arena does not hold T's halos).
         """
+        steps = GRAPH_STEPS if steps is None else int(steps)
+        if steps < 2 or steps % 2:
+            raise ValueError("Diffusion3D.capture: steps must be even and >= 2")
         if self.device.type != "cuda":
             raise RuntimeError("Diffusion3D.capture: hipGraphs need a GPU model")
         if not self._warm:
@@ -254,27 +266,29 @@ class Diffusion3D:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            self.step()
-            self.step()
+            for _ in range(steps):
+                self.step()
         torch.cuda.synchronize()
         register_graph(g)
         self.graph = g
+        self.graph_steps = steps
         self._graph_fused = self.fused
         self._graph_parity = self._fstep % 2
 
     def run(self, nt: int) -> None:
-        """Advance ``nt`` steps (by graph replays of two steps if captured)."""
+        """Advance ``nt`` steps (by graph replays of ``graph_steps`` steps if captured)."""
         if self.graph is not None and self._graph_fused == self.fused:
             # The captured fused steps have their arena halves baked in: they
             # assume a primed arena and the step-counter parity of the capture.
             while self.fused and nt > 0 and (self._fstep % 2 != self._graph_parity or not self._fprimed):
                 self.step()
                 nt -= 1
-            for _ in range(nt // 2):
+            k = self.graph_steps
+            for _ in range(nt // k):
                 self.graph.replay()
             if self.fused:
-                self._fstep += 2 * (nt // 2)
-            nt %= 2
+                self._fstep += k * (nt // k)
+            nt %= k
         for _ in range(nt):
             self.step()
 

@@ -146,7 +146,7 @@ def scenario_diffusion_fused(nx, ny, nz, steps, periodic, graph):
     a.run(steps)
     if int(graph):
         b.step()
-        b.capture()
+        b.capture(steps=2)
         b.run(steps - 1)
     else:
         b.run(steps)

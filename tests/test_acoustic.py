@@ -87,7 +87,7 @@ def test_gpu_model_graph_matches_eager(gpu):
     a, b = Acoustic2D(dtype=torch.float32), Acoustic2D(dtype=torch.float32)
     a.run(9)
     b.step()
-    b.capture()
+    b.capture(steps=4)
     b.run(8)
     torch.cuda.synchronize()
     assert torch.equal(a.P, b.P) and torch.equal(a.Vx, b.Vx)

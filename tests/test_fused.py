@@ -79,7 +79,7 @@ def test_fused_loopback_graph_and_mode_switches(gpu):
     a, b = _pair((40, 36, 72), (1, 1, 1), torch.float64, 2, loopback=True, mode=1)
     a.run(3)
     b.run(3)
-    b.capture()  # counter odd: the graph bakes in that parity
+    b.capture(steps=4)  # counter odd: the graph bakes in that parity
     a.run(8)
     b.run(8)
     b.sync_halo()
@@ -132,3 +132,23 @@ def test_fused_tiny_extents(gpu, n):
         torch.cuda.synchronize()
         assert torch.equal(a.T, b.T), (n, mode)
         igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_fused_default_graph_steps(gpu):
+    """Default capture (GRAPH_STEPS per replay) with step counts that are not
+    multiples of it, fused and plain."""
+    from igg.models.diffusion3d import GRAPH_STEPS
+
+    a, b = _pair((24, 22, 64), (1, 1, 1), torch.float64, 0)
+    c = Diffusion3D(dtype=torch.float64, variant=0)
+    a.run(2 * GRAPH_STEPS + 7)
+    b.capture()
+    c.capture()
+    assert b.graph_steps == GRAPH_STEPS and c.graph_steps == GRAPH_STEPS
+    b.run(2 * GRAPH_STEPS + 6)  # capture() ran one (priming) step
+    c.run(2 * GRAPH_STEPS + 6)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    assert torch.equal(a.T, b.T) and torch.equal(a.T, c.T)
+    igg.finalize_global_grid(finalize_MPI=False)

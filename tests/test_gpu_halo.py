@@ -213,8 +213,8 @@ def test_gpu_graph_replay_matches_eager(gpu, mode):
     b = Diffusion3D(dtype=torch.float64)
     a.run(7)
     b.step()
-    b.capture()  # graph of two steps; b has done 1 eager step
-    b.run(6)
+    b.capture(steps=4)  # graph of four steps; b has done 1 eager step
+    b.run(6)  # one replay + two eager steps
     torch.cuda.synchronize()
     assert b.graph is not None
     assert torch.equal(a.T, b.T)
@@ -249,7 +249,7 @@ def test_gpu_loopback_put_transport(gpu, monkeypatch):
     m1.run(7)
     m2.run(7)
     m3.step()
-    m3.capture()  # epoch lives on the device: replays are valid exchanges
+    m3.capture(steps=2)  # epoch lives on the device: replays are valid exchanges
     m3.run(6)
     torch.cuda.synchronize()
     assert torch.equal(m1.T, m2.T)
