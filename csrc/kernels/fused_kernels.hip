@@ -59,7 +59,9 @@ struct HxScal {
   T rdx2, rdy2, rdz2, dtlam;
 };
 
-template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF>
+// FEAT bits: 1 x-in, 2 y-in, 4 z-in, 8 z-out, 16 z-in substituted at use,
+// 64 x-out, 128 y-out (207 = the full exchange).
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
 __global__ void __launch_bounds__(64 * BY * BZ)
 diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
                       const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
@@ -105,19 +107,21 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   const T* ymb = t + (y0 - 1) * n2 + zt;
   const T* ypb = t + (y0 + nv) * n2 + zt;
   int64_t yms = s0, yps = s0;
-  if (y0 == 1 && yi0) { ymb = yi0 + zt; yms = n2; }
-  if (y0 + nv == n1 - 1 && yi1) { ypb = yi1 + zt; yps = n2; }
+  if ((FEAT & 2) && y0 == 1 && yi0) { ymb = yi0 + zt; yms = n2; }
+  if ((FEAT & 2) && y0 + nv == n1 - 1 && yi1) { ypb = yi1 + zt; yps = n2; }
   // y send rows of this wave.
-  T* const yrow0 = (y0 == 1 && yo0) ? yo0 + zt : nullptr;
+  T* const yrow0 = ((FEAT & 128) && y0 == 1 && yo0) ? yo0 + zt : nullptr;
   int ry1 = static_cast<int>(n1 - 2 - y0);
-  T* const yrow1 = (ry1 >= 0 && ry1 < nv && yo1) ? yo1 + zt : nullptr;
+  T* const yrow1 = ((FEAT & 128) && ry1 >= 0 && ry1 < nv && yo1) ? yo1 + zt : nullptr;
   if (!yrow1) ry1 = -1;
   // z edges of this wave: low edge in lane 0 (element 0 = halo z=0, element
   // 1 = send z=1), high edge in lane zh (element VZ-1 = halo, VZ-2 = send).
   const bool has_lo = zt == 0, has_hi = zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ;
-  const int zh = static_cast<int>((n2 - VZ - zt) / VZ);
-  const bool zin_lo = has_lo && zi0, zin_hi = has_hi && zi1;
-  const bool zout_lo = has_lo && zo0, zout_hi = has_hi && zo1;
+  // readfirstlane: the compiler must see zh as uniform, or every readlane
+  // with it becomes a waterfall loop draining vmcnt (measured +27 % per step).
+  const int zh = __builtin_amdgcn_readfirstlane(static_cast<int>((n2 - VZ - zt) / VZ));
+  const bool zin_lo = (FEAT & 4) && has_lo && zi0, zin_hi = (FEAT & 4) && has_hi && zi1;
+  const bool zout_lo = (FEAT & 8) && has_lo && zo0, zout_hi = (FEAT & 8) && has_hi && zo1;
   const bool zin = zin_lo || zin_hi, zout = zout_lo || zout_hi;
   const int rl = lane & 31;
   // Lane-distributed z values: row r of the low edge in lane r, of the high
@@ -135,8 +139,10 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   T* zsend_dst = nullptr;
 
   auto plane = [&](int64_t X) -> const T* {
-    if (X == 0 && xi0) return xi0;
-    if (X == n0 - 1 && xi1) return xi1;
+    if constexpr ((FEAT & 1) != 0) {
+      if (X == 0 && xi0) return xi0;
+      if (X == n0 - 1 && xi1) return xi1;
+    }
     return t + X * s0;
   };
   V tm[RY], tc[RY], tp[RY], cp[RY];
@@ -150,28 +156,31 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   const T two = T(2);
   for (int64_t x = xs; x < xe; ++x) {
     const int64_t off = x * s0;
+    // z halo of plane x (fetched one step ahead), prefetch plane x+1's.
+    [[maybe_unused]] T zcur = T(0);
     if (zin) {
-      // z halo of plane x (fetched one step ahead), prefetch plane x+1's.
-      const T zcur = znext;
+      zcur = znext;
       if (zsrc && x + 1 < xe) znext = zsrc[(x + 1) * a.zp];
+      if constexpr ((FEAT & 16) == 0) {
 #pragma unroll
-      for (int r = 0; r < RY; ++r) {
-        if (zin_lo) {
-          const T v = lane_read(zcur, r);
-          if (lane == 0) tc[r][0] = v;
-        }
-        if (zin_hi) {
-          const T v = lane_read(zcur, 32 + r);
-          if (lane == zh) tc[r][VZ - 1] = v;
+        for (int r = 0; r < RY; ++r) {
+          if (zin_lo) {
+            const T v = lane_read(zcur, r);
+            if (lane == 0) tc[r][0] = v;
+          }
+          if (zin_hi) {
+            const T v = lane_read(zcur, 32 + r);
+            if (lane == zh) tc[r][VZ - 1] = v;
+          }
         }
       }
     }
-    T* const xd0 = x == 1 ? xo0 : nullptr;
-    T* const xd1 = x == n0 - 2 ? xo1 : nullptr;
+    T* const xd0 = (FEAT & 64) && x == 1 ? xo0 : nullptr;
+    T* const xd1 = (FEAT & 64) && x == n0 - 2 ? xo1 : nullptr;
     V tn[RY], cpn[RY];
     if (PF) {
       const int64_t xn = min(x + 2, n0 - 1), xc = min(x + 1, xe - 1);
-      const T* pn = (xn == n0 - 1 && xi1) ? xi1 : t + xn * s0;
+      const T* pn = ((FEAT & 1) && xn == n0 - 1 && xi1) ? xi1 : t + xn * s0;
 #pragma unroll
       for (int r = 0; r < RY; ++r) {
         tn[r] = vld<T, VZ>(pn + rowb[r] + zl);
@@ -201,11 +210,20 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
       T next = __shfl_down(c[0], 1);
       if (load_prev) prev = em[r];
       if (load_next) next = ep[r];
+      [[maybe_unused]] T hlo = T(0), hhi = T(0);
+      if constexpr ((FEAT & 16) != 0) {  // halo substituted at its use
+        if (zin_lo) hlo = lane_read(zcur, r);
+        if (zin_hi) hhi = lane_read(zcur, 32 + r);
+      }
       V out;
 #pragma unroll
       for (int e = 0; e < VZ; ++e) {
-        const T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
-        const T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
+        T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
+        T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
+        if constexpr ((FEAT & 16) != 0) {
+          if (e == 1 && zin_lo && lane == 0) zm = hlo;
+          if (e == VZ - 2 && zin_hi && lane == zh) zp = hhi;
+        }
         const T c2 = two * c[e];
         const T lap = (tp[r][e] - c2 + tm[r][e]) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
                       (zp - c2 + zm) * a.rdz2;
@@ -257,7 +275,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
       }
     }
     if (!PF && x + 1 < xe) {
-      const T* pn = (x + 2 == n0 - 1 && xi1) ? xi1 : t + (x + 2) * s0;
+      const T* pn = ((FEAT & 1) && x + 2 == n0 - 1 && xi1) ? xi1 : t + (x + 2) * s0;
 #pragma unroll
       for (int r = 0; r < RY; ++r) {
         tp[r] = vld<T, VZ>(pn + rowb[r] + zl);
@@ -287,12 +305,12 @@ int resident(const void* kernel, int block) {
   return r;
 }
 
-template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF>
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
 void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream) {
   const int64_t n0 = d.n[0], n1 = d.n[1], n2 = d.n[2];
   if (n2 % VZ != 0 || n2 < 2 * VZ)
     fail("diffusion3d (fused halo): n2 must be a multiple of ", VZ, " and >= ", 2 * VZ);
-  auto kern = &diffusion3d_hx_kernel<T, BY, RY, VZ, PF, BZ, DF>;
+  auto kern = &diffusion3d_hx_kernel<T, BY, RY, VZ, PF, BZ, DF, FEAT>;
   const int block = 64 * BY * BZ;
   constexpr int W = 64 * VZ * BZ, TY = BY * RY;
   HxScal<T> a;
@@ -343,7 +361,31 @@ void dispatch(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hip
   }
 }
 
+// The sweep without any exchange feature (FEAT=0): the plain inner-box
+// update through this kernel's restrict-argument form, measured 13-26 us
+// faster than diffusion3d_vkernel with the same tiling (profiles/r1_fused/
+// feature_bisect_v11.log); bitwise identical arithmetic.
+template <typename T>
+void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
+  const HaloIOArgs none{};
+  switch (v) {
+    case 0: launch_hx<T, 4, 4, 4, false, 1, false, 0>(d, none, s); break;
+    case 2: launch_hx<T, 4, 4, 2, true, 1, false, 0>(d, none, s); break;
+    case 9: launch_hx<T, 4, 8, 4, false, 1, false, 0>(d, none, s); break;
+    case 11: launch_hx<T, 4, 8, 2, false, 1, false, 0>(d, none, s); break;
+    case 14: launch_hx<T, 2, 8, 4, false, 2, false, 0>(d, none, s); break;
+    default: fail("diffusion3d (restrict form): tiling ", v, " not instantiated");
+  }
+}
+
 }  // namespace
+
+void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t stream) {
+  if (a.n[0] < 3 || a.n[1] < 3 || a.n[2] < 3) fail("diffusion3d: every extent must be >= 3");
+  if (a.elem_bytes == 8) dispatch_plain<double>(a, tiling, stream);
+  else if (a.elem_bytes == 4) dispatch_plain<float>(a, tiling, stream);
+  else fail("diffusion3d: only float32/float64 are supported");
+}
 
 bool diffusion3d_fused_variant_ok(int v) {
   return v == 0 || v == 2 || v == 9 || v == 11 || v == 14;

@@ -301,7 +301,15 @@ constexpr Variant VARIANTS[] = {
     {"s_by4_ry1", 4, 1, 1, false, false},        // 18 (low-VGPR: thin send planes)
     {"v2_by4_ry1_nt", 4, 1, 2, false, true},     // 19 (low-VGPR vector)
     {"v4_by4_ry2", 4, 2, 4, false, false},       // 20
+    // 21-25: inner box through the restrict-argument kernel of fused_kernels.hip
+    // with the tiling of variant 0/2/9/11/14 (other boxes: that variant here).
+    {"hx_v4_by4_ry4_nt", 4, 4, 4, false, true},     // 21
+    {"hx_v2_by4_ry4_pf_nt", 4, 4, 2, true, true},   // 22
+    {"hx_v4_by4_ry8_nt", 4, 8, 4, false, true},     // 23
+    {"hx_v2_by4_ry8_nt", 4, 8, 2, false, true},     // 24
+    {"hx_v4_bz2_by2_ry8_nt", 2, 8, 4, false, true}, // 25
 };
+constexpr int HX_TILING[] = {0, 2, 9, 11, 14};  // variants 21..25
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
 // Grid sizing policy: `g_rounds` full residency rounds (resident workgroups =
@@ -453,6 +461,7 @@ const char* diffusion3d_variant_name(int v) {
 }
 int diffusion3d_variant_tile(int v) {
   if (v < 0 || v >= NVARIANTS) return 0;
+  if (v >= 21) v = HX_TILING[v - 21];
   const int bz = (v >= 12 && v <= 16) ? 2 : (v == 17 ? 4 : 1);
   return 64 * VARIANTS[v].vz * bz;
 }
@@ -468,6 +477,17 @@ void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, i
     for (int d = 0; d < 3; ++d)
       if (!b.empty() && (b.lo[d] < 1 || b.hi[d] > a.n[d] - 1))
         fail("diffusion3d: box outside the inner region [1, n-1) along dim ", d);
+  if (variant >= 21 && variant < NVARIANTS) {
+    const int tiling = HX_TILING[variant - 21];
+    const bool inner = boxes.size() == 1 && boxes[0].lo[0] == 1 && boxes[0].lo[1] == 1 && boxes[0].lo[2] == 1 &&
+                       boxes[0].hi[0] == a.n[0] - 1 && boxes[0].hi[1] == a.n[1] - 1 && boxes[0].hi[2] == a.n[2] - 1;
+    const int vz = VARIANTS[variant].vz;
+    if (inner && a.n[2] % vz == 0 && a.n[2] >= 2 * vz) {
+      launch_diffusion3d_inner_hx(a, tiling, stream);
+      return;
+    }
+    variant = tiling;
+  }
   if (a.elem_bytes == 8) dispatch<double>(make_args<double>(a), boxes, variant, stream);
   else if (a.elem_bytes == 4) dispatch<float>(make_args<float>(a), boxes, variant, stream);
   else fail("diffusion3d: only float32/float64 are supported");

@@ -42,7 +42,7 @@ def _run_boxes(shape, boxes, variant, dtype, gpu):
 
 @pytest.mark.parametrize("variant", range(len(stencil.variants())))
 def test_variant_full_inner_box(gpu, variant):
-    for shape in [(24, 20, 18), (37, 33, 131), (9, 70, 5)]:
+    for shape in [(24, 20, 18), (37, 33, 131), (9, 70, 5), (20, 22, 72)]:
         err, tol = _run_boxes(shape, [stencil.inner_box(shape)], variant, torch.float64, gpu)
         assert err < tol, (shape, err)
 
@@ -62,8 +62,24 @@ def test_variant_split_boxes(gpu, variant):
             assert err < tol, (act, w, boxes, err)
 
 
-@pytest.mark.parametrize("variant", [0, 11])
+@pytest.mark.parametrize("variant", [0, 11, 21, 24])
 def test_variant_float32(gpu, variant):
     shape = (40, 36, 70)
     err, tol = _run_boxes(shape, [stencil.inner_box(shape)], variant, torch.float32, gpu)
     assert err < tol
+
+
+@pytest.mark.parametrize("hx,tiling", [(21, 0), (22, 2), (23, 9), (24, 11), (25, 14)])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_restrict_form_bitwise_equals_vkernel(gpu, hx, tiling, dtype):
+    """Variants 21-25 (inner box through fused_kernels.hip without exchange
+    features) compute exactly what the stencil_kernels.hip variant with the
+    same tiling computes."""
+    shape = (26, 35, 136)
+    _, _, Tg, Cpg = _fields(shape, dtype, gpu)
+    a = torch.zeros_like(Tg)
+    b = torch.zeros_like(Tg)
+    stencil.diffusion3d_(a, Tg, Cpg, variant=tiling, **KW)
+    stencil.diffusion3d_(b, Tg, Cpg, variant=hx, **KW)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
