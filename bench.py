@@ -365,6 +365,8 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+    if hasattr(model, "close"):
+        model.close()  # collective: unmap the fused exchange's peer arenas
     igg.finalize_global_grid()
 
 

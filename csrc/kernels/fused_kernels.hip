@@ -368,12 +368,18 @@ void dispatch(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hip
 template <typename T>
 void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
   const HaloIOArgs none{};
-  switch (v) {
+  switch (v) {  // tilings: fused variants 0/2/9/11/14, then restrict-form-only ones
     case 0: launch_hx<T, 4, 4, 4, false, 1, false, 0>(d, none, s); break;
     case 2: launch_hx<T, 4, 4, 2, true, 1, false, 0>(d, none, s); break;
     case 9: launch_hx<T, 4, 8, 4, false, 1, false, 0>(d, none, s); break;
     case 11: launch_hx<T, 4, 8, 2, false, 1, false, 0>(d, none, s); break;
     case 14: launch_hx<T, 2, 8, 4, false, 2, false, 0>(d, none, s); break;
+    case 100: launch_hx<T, 2, 8, 2, false, 1, false, 0>(d, none, s); break;
+    case 101: launch_hx<T, 4, 6, 2, false, 1, false, 0>(d, none, s); break;
+    case 102: launch_hx<T, 4, 8, 2, true, 1, false, 0>(d, none, s); break;
+    case 103: launch_hx<T, 4, 4, 2, false, 1, false, 0>(d, none, s); break;
+    case 104: launch_hx<T, 4, 2, 4, false, 1, false, 0>(d, none, s); break;
+    case 105: launch_hx<T, 8, 4, 2, false, 1, false, 0>(d, none, s); break;
     default: fail("diffusion3d (restrict form): tiling ", v, " not instantiated");
   }
 }

@@ -308,8 +308,19 @@ constexpr Variant VARIANTS[] = {
     {"hx_v4_by4_ry8_nt", 4, 8, 4, false, true},     // 23
     {"hx_v2_by4_ry8_nt", 4, 8, 2, false, true},     // 24
     {"hx_v4_bz2_by2_ry8_nt", 2, 8, 4, false, true}, // 25
+    // 26-31: tilings only in the restrict form (fallback for other boxes: the
+    // nearest stencil_kernels.hip variant)
+    {"hx_v2_by2_ry8_nt", 2, 8, 2, false, true},     // 26
+    {"hx_v2_by4_ry6_nt", 4, 6, 2, false, true},     // 27
+    {"hx_v2_by4_ry8_pf_nt", 4, 8, 2, true, true},   // 28
+    {"hx_v2_by4_ry4_nt", 4, 4, 2, false, true},     // 29
+    {"hx_v4_by4_ry2_nt", 4, 2, 4, false, true},     // 30
+    {"hx_v2_by8_ry4_nt", 8, 4, 2, false, true},     // 31
 };
-constexpr int HX_TILING[] = {0, 2, 9, 11, 14};  // variants 21..25
+// Variants 21..31: restrict-form tiling id (fused_kernels.hip dispatch_plain)
+// and the stencil_kernels.hip variant used for boxes other than the inner box.
+constexpr int HX_TILING[] = {0, 2, 9, 11, 14, 100, 101, 102, 103, 104, 105};
+constexpr int HX_FALLBACK[] = {0, 2, 9, 11, 14, 11, 11, 11, 2, 5, 11};
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
 // Grid sizing policy: `g_rounds` full residency rounds (resident workgroups =
@@ -461,7 +472,7 @@ const char* diffusion3d_variant_name(int v) {
 }
 int diffusion3d_variant_tile(int v) {
   if (v < 0 || v >= NVARIANTS) return 0;
-  if (v >= 21) v = HX_TILING[v - 21];
+  if (v >= 21) v = HX_FALLBACK[v - 21];
   const int bz = (v >= 12 && v <= 16) ? 2 : (v == 17 ? 4 : 1);
   return 64 * VARIANTS[v].vz * bz;
 }
@@ -486,7 +497,7 @@ void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, i
       launch_diffusion3d_inner_hx(a, tiling, stream);
       return;
     }
-    variant = tiling;
+    variant = HX_FALLBACK[variant - 21];
   }
   if (a.elem_bytes == 8) dispatch<double>(make_args<double>(a), boxes, variant, stream);
   else if (a.elem_bytes == 4) dispatch<float>(make_args<float>(a), boxes, variant, stream);

@@ -167,6 +167,17 @@ class Diffusion3D:
             update_halo_(self.T)
             self._fprimed = False
 
+    def close(self) -> None:
+        """Release the fused exchange's peer mesh (collective: every rank)."""
+        if self._fh is not None:
+            if self.fused:
+                self.sync_halo()
+                self.fused = False
+            torch.cuda.synchronize()
+            self._fh.close()
+            self._fh = None
+            self.graph = None
+
     def check(self) -> None:
         """Raise if a fused-exchange sync kernel timed out waiting for a neighbour."""
         if self._fh is not None:

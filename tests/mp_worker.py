@@ -162,6 +162,7 @@ def scenario_diffusion_fused(nx, ny, nz, steps, periodic, graph):
     b.run(3)
     torch.cuda.synchronize()
     assert torch.equal(a.T, b.T), f"rank {me}: mismatch after leaving fused mode"
+    b.close()  # collective unmap of the peer arenas
     igg.finalize_global_grid()
     print(f"rank {me} fused OK")
 
