@@ -25,7 +25,8 @@ def run():
 
 
 res = {}
-for v, ch in [(0, 0)] + [(1, c) for c in (int(x) for x in os.environ.get("CHS", "16,32,64").split(","))]:
+chs = [int(x) for x in os.environ.get("CHS", "8,16,32,64").split(",")]
+for v, ch in [(0, 0)] + [(1, c) for c in chs] + [(2, c) for c in chs]:
     native.acoustic2d_set_variant(v)
     native.acoustic2d_set_chunk(ch)
     run()
@@ -40,6 +41,6 @@ for v, ch in [(0, 0)] + [(1, c) for c in (int(x) for x in os.environ.get("CHS", 
         ts.append(e0.elapsed_time(e1) / 10)
     ms = sorted(ts)[2]
     res[f"v{v}_ch{ch}"] = {"ms": round(ms, 4), "GBs": round(2 * (P.numel() + Vx.numel() + Vy.numel()) * P.element_size() / ms / 1e6, 1)}
-native.acoustic2d_set_variant(1)
+native.acoustic2d_set_variant(2)
 native.acoustic2d_set_chunk(0)
 print(json.dumps(res))

@@ -17,7 +17,8 @@ namespace {
 
 constexpr int BJ = 64, BI = 4;
 constexpr int WAVES = 4;       // waves per workgroup of the marching kernel
-constexpr int64_t MARCH_CH = 8;  // rows of i per wave (short chunks = more waves in flight; swept: benchmarks/acoustic_sweep.py)
+constexpr int64_t MARCH_CH = 8;   // rows of i per wave, scalar march (short chunks = more waves in flight)
+constexpr int64_t VMARCH_CH = 2;  // rows of i per wave, vector march (swept 2..12: profiles/r1_configs/acoustic_sweep_vmarch.log)
 
 template <typename T>
 struct Acc {
@@ -137,6 +138,114 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_march_kernel(AcousticAr
   }
 }
 
+// Vectorised marching version: each lane owns VJ consecutive columns (16 B
+// per lane and array for f32 VJ=4), a wave = 62 owned vectors + one halo
+// vector on each side (lanes 0 and 63), so each load/store instruction moves
+// 1 KiB instead of 256 B. Neighbour columns come from the lane's own vector or
+// one lane shuffle. P/Vx rows (pitch ny, ny % VJ == 0) are vector aligned; Vy
+// rows have pitch ny+1, so Vy uses element-aligned vector accesses (gfx950
+// global memory accepts dword-aligned dwordx4), and the lane that starts at
+// column ny handles the last Vy face column with a scalar access. Same
+// arithmetic per element as acoustic2d_march_kernel (bitwise equal).
+template <typename T, int VJ>
+__global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticArgs a, int64_t ch) {
+  typedef T V __attribute__((ext_vector_type(VJ)));
+  typedef T VU __attribute__((ext_vector_type(VJ), aligned(sizeof(T))));
+  constexpr int64_t OWNV = 62 * VJ;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nx = a.nx, ny = a.ny, sy = ny + 1;
+  const int64_t nseg = (ny + 1 + OWNV - 1) / OWNV;
+  const int64_t seg = wave % nseg, chunk = wave / nseg;
+  const int64_t i0 = chunk * ch;
+  if (i0 > nx) return;  // wave-uniform
+  const int64_t i1 = min(i0 + ch, nx + 1);
+  const int64_t j0 = seg * OWNV + static_cast<int64_t>(lane - 1) * VJ;  // first column of this lane
+  const bool own = lane >= 1 && lane <= 62 && j0 <= ny;
+  const bool cells = j0 + VJ <= ny && j0 >= 0;   // VJ cell / x-face columns
+  const bool last = j0 == ny;                    // only the boundary y-face column ny
+  const int64_t jl = min<int64_t>(max<int64_t>(j0, 0), ny - VJ);  // clamped vector start
+  const T* __restrict__ p = reinterpret_cast<const T*>(a.p);
+  const T* __restrict__ vx = reinterpret_cast<const T*>(a.vx);
+  const T* __restrict__ vy = reinterpret_cast<const T*>(a.vy);
+  T* __restrict__ p2 = reinterpret_cast<T*>(a.p2);
+  T* __restrict__ vx2 = reinterpret_cast<T*>(a.vx2);
+  T* __restrict__ vy2 = reinterpret_cast<T*>(a.vy2);
+  const T dtk = static_cast<T>(a.dtk), dt_rho = static_cast<T>(a.dt_rho);
+  const T rdx = static_cast<T>(a.rdx), rdy = static_cast<T>(a.rdy);
+  auto ldv = [&](const T* base, int64_t row) { return *reinterpret_cast<const V*>(base + row * ny + jl); };
+  auto ldy = [&](int64_t row) {  // Vy(row, j0..j0+VJ-1); the column-ny lane holds Vy(row, ny) in element 0
+    V v = *reinterpret_cast<const VU*>(vy + row * sy + jl);
+    if (last) {
+      v = V(T(0));
+      v[0] = vy[row * sy + ny];
+    }
+    return v;
+  };
+  auto vy_next = [&](const V& h) {  // Vy(row, j+1) per element
+    V n;
+    const T up = __shfl_down(h[0], 1);
+#pragma unroll
+    for (int e = 0; e < VJ; ++e) n[e] = e + 1 < VJ ? h[e + 1 < VJ ? e + 1 : e] : up;
+    return n;
+  };
+  V vx_i = ldv(vx, i0);
+  V p2_prev = V(T(0));
+  if (i0 >= 1) {
+    const V vyh = ldy(i0 - 1), vxp = ldv(vx, i0 - 1), pp0 = ldv(p, i0 - 1);
+    const V vyn = vy_next(vyh);
+#pragma unroll
+    for (int e = 0; e < VJ; ++e) p2_prev[e] = pp0[e] - dtk * ((vx_i[e] - vxp[e]) * rdx + (vyn[e] - vyh[e]) * rdy);
+  }
+  V vy_h = V(T(0)), vx_n = V(T(0)), pp = V(T(0));
+  if (i0 < nx) {
+    vy_h = ldy(i0);
+    vx_n = ldv(vx, i0 + 1);
+    pp = ldv(p, i0);
+  }
+  for (int64_t i = i0; i < i1; ++i) {
+    if (i < nx) {
+      V vy_h1 = V(T(0)), vx_n1 = V(T(0)), pp1 = V(T(0));
+      if (i + 1 < nx && i + 1 < i1) {  // prefetch row i+1
+        vy_h1 = ldy(i + 1);
+        vx_n1 = ldv(vx, i + 2);
+        pp1 = ldv(p, i + 1);
+      }
+      const V vy_n = vy_next(vy_h);
+      V pc;
+#pragma unroll
+      for (int e = 0; e < VJ; ++e) pc[e] = pp[e] - dtk * ((vx_n[e] - vx_i[e]) * rdx + (vy_n[e] - vy_h[e]) * rdy);
+      const T pl_lane = __shfl_up(pc[VJ - 1], 1);
+      if (own) {
+        V vyo;
+#pragma unroll
+        for (int e = 0; e < VJ; ++e) {
+          const T pl = e == 0 ? pl_lane : pc[e > 0 ? e - 1 : 0];
+          const int64_t j = j0 + e;
+          vyo[e] = (j >= 1 && j <= ny - 1) ? vy_h[e] - dt_rho * (pc[e] - pl) * rdy : vy_h[e];
+        }
+        if (cells) {
+          V vxo;
+#pragma unroll
+          for (int e = 0; e < VJ; ++e) vxo[e] = (i >= 1) ? vx_i[e] - dt_rho * (pc[e] - p2_prev[e]) * rdx : vx_i[e];
+          __builtin_nontemporal_store(pc, reinterpret_cast<V*>(p2 + i * ny + j0));
+          __builtin_nontemporal_store(vxo, reinterpret_cast<V*>(vx2 + i * ny + j0));
+          *reinterpret_cast<VU*>(vy2 + i * sy + j0) = vyo;
+        } else if (last) {
+          vy2[i * sy + ny] = vy_h[0];
+        }
+      }
+      vx_i = vx_n;
+      p2_prev = pc;
+      vy_h = vy_h1;
+      vx_n = vx_n1;
+      pp = pp1;
+    } else if (own && cells) {  // i == nx: the last x-faces are boundary faces
+      *reinterpret_cast<V*>(vx2 + i * ny + j0) = vx_i;
+    }
+  }
+}
+
 template <typename T>
 void host_typed(const AcousticArgs& a) {
   const int64_t nx = a.nx, ny = a.ny;
@@ -171,17 +280,28 @@ void host_typed(const AcousticArgs& a) {
 
 }  // namespace
 
-static int g_acoustic_variant = 1;  // 0: one thread per cell (recompute), 1: marching
-static int64_t g_march_ch = MARCH_CH;
+static int g_acoustic_variant = 2;  // 0: one thread per cell (recompute), 1: marching, 2: vector marching
+static int64_t g_march_ch = 0;  // 0: the variant's default
 void acoustic2d_set_variant(int v) { g_acoustic_variant = v; }
-void acoustic2d_set_chunk(int64_t ch) { g_march_ch = ch > 0 ? ch : MARCH_CH; }
+void acoustic2d_set_chunk(int64_t ch) { g_march_ch = ch > 0 ? ch : 0; }
 
 void launch_acoustic2d(const AcousticArgs& a, hipStream_t stream) {
   if (a.nx < 1 || a.ny < 1) fail("acoustic2d: empty grid");
   if (a.elem_bytes != 4 && a.elem_bytes != 8)
     fail("acoustic2d: element size must be 4 or 8 bytes (got ", a.elem_bytes, ")");
-  if (g_acoustic_variant == 1) {
-    const int64_t ch = g_march_ch;
+  constexpr int VJ4 = 4, VJ8 = 2;  // 16 B per lane (f32 / f64)
+  const int vj = a.elem_bytes == 4 ? VJ4 : VJ8;
+  if (g_acoustic_variant == 2 && a.ny % vj == 0 && a.ny >= 2 * vj) {
+    const int64_t ch = g_march_ch > 0 ? g_march_ch : VMARCH_CH;
+    const int64_t nseg = (a.ny + 1 + 62 * vj - 1) / (62 * vj), nch = (a.nx + 1 + ch - 1) / ch;
+    const int64_t waves = nseg * nch;
+    const dim3 grid(static_cast<unsigned>((waves + WAVES - 1) / WAVES));
+    if (a.elem_bytes == 8)
+      hipLaunchKernelGGL((acoustic2d_vmarch_kernel<double, VJ8>), grid, dim3(64 * WAVES), 0, stream, a, ch);
+    else
+      hipLaunchKernelGGL((acoustic2d_vmarch_kernel<float, VJ4>), grid, dim3(64 * WAVES), 0, stream, a, ch);
+  } else if (g_acoustic_variant >= 1) {
+    const int64_t ch = g_march_ch > 0 ? g_march_ch : MARCH_CH;
     const int64_t nseg = (a.ny + 1 + OWN - 1) / OWN, nch = (a.nx + 1 + ch - 1) / ch;
     const int64_t waves = nseg * nch;
     const dim3 grid(static_cast<unsigned>((waves + WAVES - 1) / WAVES));

@@ -60,9 +60,9 @@ def test_multirank_matches_global(nprocs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-13), (torch.float32, 2e-6)])
-@pytest.mark.parametrize("shape", [(130, 257), (64, 63), (200, 64), (3, 2)])
+@pytest.mark.parametrize("shape", [(130, 257), (64, 63), (200, 64), (3, 2), (130, 256), (17, 1000), (5, 8)])
 def test_gpu_step_matches_reference(gpu, variant, dtype, tol, shape):
     P, Vx, Vy = _fields(*shape, dtype, gpu)
     native.acoustic2d_set_variant(variant)
@@ -70,7 +70,7 @@ def test_gpu_step_matches_reference(gpu, variant, dtype, tol, shape):
         got = _step(P, Vx, Vy, True, **KW)
         torch.cuda.synchronize()
     finally:
-        native.acoustic2d_set_variant(1)
+        native.acoustic2d_set_variant(2)
     ref = acoustic2d_reference(P.cpu(), Vx.cpu(), Vy.cpu(), **KW)
     for g, r in zip(got, ref):
         assert (g.cpu().double() - r).abs().max().item() < tol
@@ -92,3 +92,23 @@ def test_gpu_model_graph_matches_eager(gpu):
     torch.cuda.synchronize()
     assert torch.equal(a.P, b.P) and torch.equal(a.Vx, b.Vx)
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("shape", [(300, 1024), (64, 520), (9, 16)])
+def test_gpu_vector_march_bitwise_equals_march(gpu, dtype, shape):
+    """Variant 2 (16 B per lane) evaluates the same expressions as variant 1
+    (up to the compiler's FMA contraction choices: a few ulp)."""
+    P, Vx, Vy = _fields(*shape, dtype, gpu)
+    out = []
+    for v in (1, 2):
+        native.acoustic2d_set_variant(v)
+        try:
+            out.append(_step(P, Vx, Vy, True, **KW))
+            torch.cuda.synchronize()
+        finally:
+            native.acoustic2d_set_variant(2)
+    eps = torch.finfo(dtype).eps
+    for a, b in zip(*out):
+        assert torch.allclose(a, b, rtol=8 * eps, atol=8 * eps)
