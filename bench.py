@@ -114,16 +114,19 @@ def select_transport(model, field, comm, log, ref: str = "rccl") -> tuple[str, d
     A, B = field.clone(), field.clone()
     H.set_transport(ref)
     H.update_halo_(A)
-    H.set_transport("put")
-    H.update_halo_(B)
-    torch.cuda.synchronize()
-    ok = bool(torch.equal(A, B))
+    ok = False
     try:
+        H.set_transport("put")  # collective: raises on every rank if a peer cannot be mapped
+        H.update_halo_(B)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(A, B))
         H.check_transport()
-    except Exception as e:  # a bounded spin timed out: the put path does not work here
-        log(f"put transport failed its check: {e}")
-        comm.mesh.clear_error()
+    except Exception as e:  # no IPC mapping, or a bounded spin timed out: put does not work here
+        log(f"put transport failed its check: {type(e).__name__}: {e}"[:300])
+        if getattr(comm, "mesh", None) is not None:
+            comm.mesh.clear_error()
         ok = False
+        H.set_transport(ref)
     bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
     del A, B
     times = {}

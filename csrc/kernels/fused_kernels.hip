@@ -59,8 +59,9 @@ struct HxScal {
   T rdx2, rdy2, rdz2, dtlam;
 };
 
-// FEAT bits: 1 x-in, 2 y-in, 4 z-in, 8 z-out, 16 z-in substituted at use,
-// 64 x-out, 128 y-out (207 = the full exchange).
+// FEAT bits (compile-time exchange features): 1 x-in, 2 y-in, 4 z-in, 8 z-out,
+// 64 x-out, 128 y-out. 207 = the full exchange, 0 = the plain update (variants
+// 21+); other subsets served the cost bisect (profiles/r1_fused/feature_bisect_*).
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
 __global__ void __launch_bounds__(64 * BY * BZ)
 diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
@@ -74,7 +75,13 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   const int64_t tz = b % a.ntz;
   const int64_t rest = b / a.ntz;
   const int64_t ty = rest % a.nty;
-  const int64_t cx = rest / a.nty;
+  // Chunks holding the x send planes run first (order 0, last, 1, 2, ...): the
+  // plane x=n0-2 is computed in the last step of the last chunk, so with >= 2
+  // residency rounds its remote stores drain while later rounds compute
+  // instead of at the kernel's tail. Scheduling only: results are unchanged.
+  const int64_t nch = (a.n0 - 2 + a.ch - 1) / a.ch;
+  const int64_t cxr = rest / a.nty;
+  const int64_t cx = (cxr == 0 || nch < 2) ? cxr : (cxr == 1 ? nch - 1 : cxr - 1);
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wz = wid % BZ, wy = wid / BZ;
@@ -156,22 +163,21 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   const T two = T(2);
   for (int64_t x = xs; x < xe; ++x) {
     const int64_t off = x * s0;
-    // z halo of plane x (fetched one step ahead), prefetch plane x+1's.
-    [[maybe_unused]] T zcur = T(0);
+    // z halo of plane x (fetched one step ahead), prefetch plane x+1's. (The
+    // alternative of substituting it at its use measured slower for every
+    // tiling: profiles/r1_fused/feature_bisect_v11_zin_alt.log.)
     if (zin) {
-      zcur = znext;
+      const T zcur = znext;
       if (zsrc && x + 1 < xe) znext = zsrc[(x + 1) * a.zp];
-      if constexpr ((FEAT & 16) == 0) {
 #pragma unroll
-        for (int r = 0; r < RY; ++r) {
-          if (zin_lo) {
-            const T v = lane_read(zcur, r);
-            if (lane == 0) tc[r][0] = v;
-          }
-          if (zin_hi) {
-            const T v = lane_read(zcur, 32 + r);
-            if (lane == zh) tc[r][VZ - 1] = v;
-          }
+      for (int r = 0; r < RY; ++r) {
+        if (zin_lo) {
+          const T v = lane_read(zcur, r);
+          if (lane == 0) tc[r][0] = v;
+        }
+        if (zin_hi) {
+          const T v = lane_read(zcur, 32 + r);
+          if (lane == zh) tc[r][VZ - 1] = v;
         }
       }
     }
@@ -210,20 +216,11 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
       T next = __shfl_down(c[0], 1);
       if (load_prev) prev = em[r];
       if (load_next) next = ep[r];
-      [[maybe_unused]] T hlo = T(0), hhi = T(0);
-      if constexpr ((FEAT & 16) != 0) {  // halo substituted at its use
-        if (zin_lo) hlo = lane_read(zcur, r);
-        if (zin_hi) hhi = lane_read(zcur, 32 + r);
-      }
       V out;
 #pragma unroll
       for (int e = 0; e < VZ; ++e) {
-        T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
-        T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
-        if constexpr ((FEAT & 16) != 0) {
-          if (e == 1 && zin_lo && lane == 0) zm = hlo;
-          if (e == VZ - 2 && zin_hi && lane == zh) zp = hhi;
-        }
+        const T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
+        const T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
         const T c2 = two * c[e];
         const T lap = (tp[r][e] - c2 + tm[r][e]) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
                       (zp - c2 + zm) * a.rdz2;

@@ -69,16 +69,28 @@ void PeerMesh::exchange_handles(bool flags_too) {
   const std::vector<std::string> all = allgather_(mine);
   if (static_cast<int>(all.size()) != nranks_) fail("PeerMesh: allgather returned ", all.size(), " entries");
   const size_t hb = sizeof(hipIpcMemHandle_t);
-  for (int r = 0; r < nranks_; ++r) {
-    if (r == rank_) continue;
-    const std::string& h = all[r];
-    size_t pos = 0;
-    if (flags_too) {
-      peer_flags_[r] = static_cast<uint64_t*>(ipc_open(h.substr(pos, hb)));
-      pos += hb;
+  std::string error;
+  try {
+    for (int r = 0; r < nranks_; ++r) {
+      if (r == rank_) continue;
+      const std::string& h = all[r];
+      size_t pos = 0;
+      if (flags_too) {
+        peer_flags_[r] = static_cast<uint64_t*>(ipc_open(h.substr(pos, hb)));
+        pos += hb;
+      }
+      if (arena_) peer_arena_[r] = static_cast<char*>(ipc_open(h.substr(pos, hb)));
     }
-    if (arena_) peer_arena_[r] = static_cast<char*>(ipc_open(h.substr(pos, hb)));
+  } catch (const Error& e) {
+    error = e.what();
   }
+  // Agree on the outcome: a rank that cannot map its peers must not leave the
+  // others waiting in the next collective, so every rank raises together.
+  const std::vector<std::string> status = allgather_(error.empty() ? std::string("1") : std::string("0"));
+  for (int r = 0; r < static_cast<int>(status.size()); ++r)
+    if (status[r] != "1")
+      fail("PeerMesh: rank ", r, " could not map the peer memory of the mesh",
+           error.empty() ? std::string() : std::string(" (here: ") + error + ")");
 }
 
 void PeerMesh::ensure_arena(size_t bytes) {
