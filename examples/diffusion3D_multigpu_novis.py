@@ -24,15 +24,22 @@ def main():
     ap.add_argument("--nx", type=int, default=256)
     ap.add_argument("--nt", type=int, default=1000)
     ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--fused", action="store_true",
+                    help="exchange halos from inside the stencil kernel (peer stores over xGMI) instead of update_halo_")
     a = ap.parse_args()
     import torch
 
     me, dims, nprocs, coords, comm = igg.init_global_grid(a.nx, a.nx, a.nx)  # Initialize the implicit global grid
     model = Diffusion3D(dtype=getattr(torch, a.dtype))                       # lam=1, cp_min=1, l=10, Gaussian ICs
+    if a.fused:
+        model.set_fused(True)                                                # collective; no-op without neighbours
     model.run(10)                                                            # warm-up (kernel variant, buffers)
+    model.capture()                                                          # hipGraph of GRAPH_STEPS steps
     igg.tic()
     model.run(a.nt)
     t = igg.toc()
+    model.sync_halo()                                                        # halos of T valid again (fused mode)
+    model.close()
     if me == 0:
         t_it = t / a.nt
         print(f"{nprocs} process(es) {dims.tolist()}, local {a.nx}^3, global {igg.nx_g()}x{igg.ny_g()}x{igg.nz_g()}: "

@@ -42,6 +42,7 @@ def test_acoustic_multicpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_diffusion_multigpu_novis():
-    out = _run([os.path.join(EX, "diffusion3D_multigpu_novis.py"), "--nx", "64", "--nt", "20"])
+@pytest.mark.parametrize("extra", [[], ["--fused"]])
+def test_diffusion_multigpu_novis(extra):
+    out = _run([os.path.join(EX, "diffusion3D_multigpu_novis.py"), "--nx", "64", "--nt", "20"] + extra)
     assert "T_eff" in out
