@@ -60,7 +60,7 @@ struct HxScal {
 };
 
 // FEAT bits (compile-time exchange features): 1 x-in, 2 y-in, 4 z-in, 8 z-out,
-// 64 x-out, 128 y-out. 207 = the full exchange, 0 = the plain update (variants
+// 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants). 207 = the full exchange, 0 = the plain update (variants
 // 21+); other subsets served the cost bisect (profiles/r1_fused/feature_bisect_*).
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
 __global__ void __launch_bounds__(64 * BY * BZ)
@@ -152,13 +152,19 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     }
     return t + X * s0;
   };
+  // Cp is streamed once (no reuse): FEAT bit 256 loads it non-temporally so it
+  // does not displace the T lines that neighbouring waves re-read (y/z halos).
+  auto ldc = [&](const T* p) -> V {
+    if constexpr ((FEAT & 256) != 0) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+    return vld<T, VZ>(p);
+  };
   V tm[RY], tc[RY], tp[RY], cp[RY];
 #pragma unroll
   for (int r = 0; r < RY; ++r) {
     tm[r] = vld<T, VZ>(plane(xs - 1) + rowb[r] + zl);
     tc[r] = vld<T, VZ>(plane(xs) + rowb[r] + zl);
     tp[r] = vld<T, VZ>(plane(xs + 1) + rowb[r] + zl);
-    cp[r] = vld<T, VZ>(cpp + xs * s0 + rowb[r] + zl);
+    cp[r] = ldc(cpp + xs * s0 + rowb[r] + zl);
   }
   const T two = T(2);
   for (int64_t x = xs; x < xe; ++x) {
@@ -190,7 +196,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
 #pragma unroll
       for (int r = 0; r < RY; ++r) {
         tn[r] = vld<T, VZ>(pn + rowb[r] + zl);
-        cpn[r] = vld<T, VZ>(cpp + xc * s0 + rowb[r] + zl);
+        cpn[r] = ldc(cpp + xc * s0 + rowb[r] + zl);
       }
     }
     const V ym = vld<T, VZ>(ymb + x * yms + zl);
@@ -276,7 +282,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
 #pragma unroll
       for (int r = 0; r < RY; ++r) {
         tp[r] = vld<T, VZ>(pn + rowb[r] + zl);
-        cp[r] = vld<T, VZ>(cpp + (x + 1) * s0 + rowb[r] + zl);
+        cp[r] = ldc(cpp + (x + 1) * s0 + rowb[r] + zl);
       }
     }
   }
@@ -377,6 +383,10 @@ void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
     case 103: launch_hx<T, 4, 4, 2, false, 1, false, 0>(d, none, s); break;
     case 104: launch_hx<T, 4, 2, 4, false, 1, false, 0>(d, none, s); break;
     case 105: launch_hx<T, 8, 4, 2, false, 1, false, 0>(d, none, s); break;
+    case 110: launch_hx<T, 4, 8, 2, false, 1, false, 256>(d, none, s); break;  // + non-temporal Cp
+    case 111: launch_hx<T, 4, 4, 4, false, 1, false, 256>(d, none, s); break;
+    case 112: launch_hx<T, 4, 8, 4, false, 1, false, 256>(d, none, s); break;
+    case 113: launch_hx<T, 2, 8, 4, false, 2, false, 256>(d, none, s); break;
     default: fail("diffusion3d (restrict form): tiling ", v, " not instantiated");
   }
 }

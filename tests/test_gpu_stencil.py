@@ -69,7 +69,8 @@ def test_variant_float32(gpu, variant):
     assert err < tol
 
 
-@pytest.mark.parametrize("hx,tiling", [(21, 0), (22, 2), (23, 9), (24, 11), (25, 14)])
+@pytest.mark.parametrize("hx,tiling", [(21, 0), (22, 2), (23, 9), (24, 11), (25, 14), (32, 11), (33, 0), (34, 9),
+                                       (35, 14)])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_restrict_form_bitwise_equals_vkernel(gpu, hx, tiling, dtype):
     """Variants 21-25 (inner box through fused_kernels.hip without exchange
