@@ -230,6 +230,49 @@ def scenario_gather_async():
     print(f"rank {me} gather_async OK")
 
 
+def scenario_fused_soak(nx, ny, nz, rounds, per_round):
+    """Fused exchange under load: ``rounds`` x ``per_round`` graph-replayed
+    fused steps with random host-side delays between rounds (ranks drift
+    apart; the device-side neighbour barrier must absorb it), odd step counts
+    (eager steps re-align the captured parity) and a sync_halo every few
+    rounds; compared bitwise with stencil + update_halo_ at the end."""
+    import random
+    import time
+
+    from igg.models.diffusion3d import Diffusion3D
+
+    device = _device("gpu")
+    nx, ny, nz, rounds, per_round = int(nx), int(ny), int(nz), int(rounds), int(per_round)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, periodx=1, periody=1, periodz=1,
+                                                          quiet=True, select_device=False)
+    v = int(os.environ.get("IGG_TEST_VARIANT", "0"))
+    a = Diffusion3D(dtype=torch.float64, device=device, variant=v)
+    b = Diffusion3D(dtype=torch.float64, device=device, variant=v)
+    b.fused_variant, b.fused_mode = v, int(os.environ.get("IGG_TEST_FUSED_MODE", "0"))
+    assert b.set_fused(True)
+    b.step()
+    b.capture(steps=4)
+    rng = random.Random(1234 + me)
+    total = 1  # steps b has done
+    for k in range(rounds):
+        time.sleep(rng.random() * 0.02)  # host skew: this rank enqueues late
+        n = per_round + (k % 3)  # odd and even counts
+        b.run(n)
+        total += n
+        if k % 7 == 6:
+            b.sync_halo()
+    a.run(total)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    if not torch.equal(a.T, b.T):
+        bad = (a.T != b.T).nonzero()[:5].tolist()
+        raise AssertionError(f"rank {me}: fused soak differs after {total} steps at {bad}")
+    b.close()
+    igg.finalize_global_grid()
+    print(f"rank {me} fused soak OK ({total} steps)")
+
+
 def scenario_put_timeout():
     """Rank 1 skips one update_halo_: rank 0's bounded waits expire (short
     IGG_PUT_TIMEOUT), its kernels exit, and check_transport reports it."""

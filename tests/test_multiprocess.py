@@ -117,3 +117,12 @@ def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
     # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
     run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=200)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,kernel", [(4, ("0", "0")), (8, ("0", "1"))])
+def test_fused_soak_with_rank_skew(nprocs, kernel):
+    """Thousands of graph-replayed fused steps with random host skew between
+    ranks stay bitwise equal to stencil + update_halo_."""
+    env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "30", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
+    run_ranks(nprocs, "fused_soak", 20, 18, 32, 60, 40, env_extra=env, timeout=300)
