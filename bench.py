@@ -10,18 +10,20 @@ per-N values). ``value`` is the WHOLE-JOB aggregate T_eff (sum over GPUs).
 
 One process per GPU (torchrun); each rank owns a 512^3 block; the process
 topology comes from init_global_grid (2 GPUs -> 2x1x1, 4 -> 2x2x1,
-8 -> 2x2x2); every step = fused stencil + update_halo_ (serial by default:
-on MI355X the boundary/interior split costs more than the ~40 us exchange).
+8 -> 2x2x2); every step = fused stencil + halo exchange: update_halo_ after
+the stencil, or the fused exchange from inside the stencil kernel (below).
 
 Multi-GPU: ``--transport auto`` (default) checks that the one-sided put
 transport reproduces the RCCL exchange bitwise on this node, times a few steps
 with each (MAX over ranks) during warm-up and keeps the faster; the timed
-steps are replayed from a hipGraph (two steps per replay) unless --no-graph.
+steps are replayed from a hipGraph (GRAPH_STEPS=10 steps per replay) unless
+--no-graph.
 
 ``--fused auto`` (default; diffusion3d with neighbours): the stencil kernel
 itself stores its send planes into the neighbours' IPC-mapped arenas over xGMI
 and a 1-wave kernel synchronises (igg/fused.hpp) — checked bitwise against the
-update_halo_ schedule on every rank, then A/B-timed; the faster is kept.
+update_halo_ schedule on every rank over 24 graph-replayed steps, then A/B-timed
+(tiling x send mode x grid rounds); the faster schedule is kept.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n 512]
                        [--dtype float64] [--overlap] [--variant V|auto]
@@ -72,7 +74,7 @@ def parse():
     ap.add_argument("--loopback", action="store_true",
                     help="1 GPU: route all 6 faces through the RCCL remote path to itself (interior-rank emulation)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
-                    help="replay the step as a hipGraph (two captured steps per replay; default)")
+                    help="replay the steps from a hipGraph (GRAPH_STEPS captured steps per replay; default)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "put"],
                     help="device transport of the halo exchange (multi-GPU / loopback)")
@@ -155,22 +157,28 @@ def select_transport(model, field, comm, log, ref: str = "rccl") -> tuple[str, d
 
 def select_fused(model, comm, log, mode: str) -> dict | None:
     """Fused halo exchange (stencil stores the send planes into the neighbours'
-    arenas; igg/fused.hpp) vs the schedule chosen so far: bitwise check of 4
+    arenas; igg/fused.hpp) vs the schedule chosen so far: bitwise check of 24
     steps from the same state on every rank, then A/B timing (MAX over ranks).
     ``mode``: auto (keep the faster), on (force when it checks out), off."""
     import torch
 
     if mode == "off" or not getattr(model, "can_fuse", False):
         return None
+    # Same execution shape as the timed run: a primed arena, hipGraph replays of
+    # captured fused steps (plus eager steps for the parity), 24 steps.
+    nchk = 24
     T0, T20 = model.T.clone(), model.T2.clone()
-    model.run(4)
+    model.run(nchk)
     ref = model.T.clone()
     model.T.copy_(T0)
     model.T2.copy_(T20)
     ok = False
     try:
         model.set_fused(True)
-        model.run(4)
+        model.step()
+        model.capture(steps=4)
+        model.run(nchk - 1)
+        model.graph = None
         model.sync_halo()
         torch.cuda.synchronize()
         model.check()
