@@ -26,11 +26,12 @@ from .parallel.device import select_device  # noqa: F401
 from .parallel.halo import update_halo, update_halo_  # noqa: F401
 from .parallel.gather import gather, gather_, gather_async_  # noqa: F401
 from .utils.tools import coords_g, nx_g, ny_g, nz_g, tic, toc, x_g, y_g, z_g  # noqa: F401
+from .utils.checkpoint import load_checkpoint, save_checkpoint  # noqa: F401
 
 __version__ = "0.1.0"
 
 __all__ = [
     "init_global_grid", "finalize_global_grid", "update_halo_", "update_halo", "gather_", "gather",
     "select_device", "nx_g", "ny_g", "nz_g", "x_g", "y_g", "z_g", "tic", "toc", "get_global_grid",
-    "IGGError", "coords_g", "gather_async_",
+    "IGGError", "coords_g", "gather_async_", "save_checkpoint", "load_checkpoint",
 ]

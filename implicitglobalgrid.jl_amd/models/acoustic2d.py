@@ -98,6 +98,27 @@ class Acoustic2D:
         for _ in range(nt):
             self.step()
 
+    def save(self, prefix: str, step: int = 0) -> str:
+        """Per-rank checkpoint of the model state (collective; utils.checkpoint)."""
+        from ..utils.checkpoint import save_checkpoint
+
+        return save_checkpoint(prefix, step=step, P=self.P, Vx=self.Vx, Vy=self.Vy, P2=self.P2, Vx2=self.Vx2,
+                               Vy2=self.Vy2)
+
+    def restore(self, prefix: str) -> int:
+        """Load a checkpoint written by ``save`` on the same decomposition (in
+        place); returns the saved step."""
+        from ..utils.checkpoint import load_checkpoint
+
+        meta, f = load_checkpoint(prefix, device=self.device)
+        for name in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2"):
+            dst = getattr(self, name)
+            if f[name].shape != dst.shape or f[name].dtype != dst.dtype:
+                raise ValueError(f"Acoustic2D.restore: {name} is {tuple(f[name].shape)}/{f[name].dtype}, "
+                                 f"the model has {tuple(dst.shape)}/{dst.dtype}")
+            dst.copy_(f[name])
+        return int(meta["step"])
+
     @property
     def a_eff_bytes(self) -> int:
         """Each of P, Vx, Vy read once and written once per step."""

@@ -178,6 +178,30 @@ class Diffusion3D:
             self._fh = None
             self.graph = None
 
+    def save(self, prefix: str, step: int = 0) -> str:
+        """Per-rank checkpoint of the model state (collective; utils.checkpoint).
+        Materialises fused-mode halos first, so the files hold consistent fields."""
+        from ..utils.checkpoint import save_checkpoint
+
+        self.sync_halo()
+        return save_checkpoint(prefix, step=step, T=self.T, T2=self.T2, Cp=self.Cp)
+
+    def restore(self, prefix: str) -> int:
+        """Load a checkpoint written by ``save`` on the same decomposition into
+        the model's buffers (in place: captured graphs stay valid); returns the
+        saved step."""
+        from ..utils.checkpoint import load_checkpoint
+
+        meta, f = load_checkpoint(prefix, device=self.device)
+        for name in ("T", "T2", "Cp"):
+            dst = getattr(self, name)
+            if f[name].shape != dst.shape or f[name].dtype != dst.dtype:
+                raise ValueError(f"Diffusion3D.restore: {name} is {tuple(f[name].shape)}/{f[name].dtype}, "
+                                 f"the model has {tuple(dst.shape)}/{dst.dtype}")
+            dst.copy_(f[name])
+        self._fprimed = False  # the fused arena does not hold these halos; T's own halo planes do
+        return int(meta["step"])
+
     def check(self) -> None:
         """Raise if a fused-exchange sync kernel timed out waiting for a neighbour."""
         if self._fh is not None:

@@ -273,6 +273,34 @@ def scenario_fused_soak(nx, ny, nz, rounds, per_round):
     print(f"rank {me} fused soak OK ({total} steps)")
 
 
+def scenario_checkpoint(dev, model, tmpdir):
+    """Run 6 steps, checkpoint, run 5 more; a fresh model restored from the
+    checkpoint and run 5 steps must match bitwise (per rank)."""
+    from igg.models.acoustic2d import Acoustic2D
+    from igg.models.diffusion3d import Diffusion3D
+
+    device = _device(dev)
+    is2d = model == "acoustic"
+    me, dims, nprocs, coords, comm = igg.init_global_grid(18, 16, 1 if is2d else 14, periodx=1, quiet=True,
+                                                          select_device=False,
+                                                          device_type="AMDGPU" if dev == "gpu" else "none")
+    make = (lambda: Acoustic2D(dtype=torch.float64, device=device)) if is2d else \
+        (lambda: Diffusion3D(dtype=torch.float64, device=device))
+    a = make()
+    a.run(6)
+    prefix = os.path.join(tmpdir, "ckpt")
+    a.save(prefix, step=6)
+    a.run(5)
+    b = make()
+    assert b.restore(prefix) == 6
+    b.run(5)
+    names = ("P", "Vx", "Vy") if is2d else ("T",)
+    for n in names:
+        assert torch.equal(getattr(a, n), getattr(b, n)), f"rank {me}: {n} differs after restart"
+    igg.finalize_global_grid()
+    print(f"rank {me} checkpoint OK")
+
+
 def scenario_put_timeout():
     """Rank 1 skips one update_halo_: rank 0's bounded waits expire (short
     IGG_PUT_TIMEOUT), its kernels exit, and check_transport reports it."""
