@@ -84,3 +84,41 @@ def test_restrict_form_bitwise_equals_vkernel(gpu, hx, tiling, dtype):
     stencil.diffusion3d_(b, Tg, Cpg, variant=hx, **KW)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+def _nan_padded(shape, dtype, gpu, src, pad=4096):
+    """A view of ``src`` in the middle of a buffer filled with NaN: any read
+    outside the array that leaks into a stored value shows up as NaN."""
+    n = src.numel()
+    buf = torch.full((n + 2 * pad,), float("nan"), dtype=dtype, device=gpu)
+    v = buf[pad:pad + n].view(shape)
+    v.copy_(src)
+    return v
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_variants_ignore_memory_around_arrays(gpu, dtype):
+    """Kernels never let a value from outside T / Cp (e.g. the gaps of the
+    model's carved buffer) reach a stored cell, for every variant, grid-rounds
+    setting and the boundary-slab / interior boxes of the overlapped step."""
+    bad = []
+    for shape in [(40, 33, 70), (37, 33, 131), (24, 20, 18), (9, 70, 5), (20, 22, 72)]:
+        T, Cp, Tg, Cpg = _fields(shape, dtype, gpu)
+        Tn, Cpn = _nan_padded(shape, dtype, gpu, Tg), _nan_padded(shape, dtype, gpu, Cpg)
+        ref = stencil.diffusion3d_reference(Tg.double().cpu(), Cpg.double().cpu(), **KW)
+        slabs, interior = stencil.split_boundary(shape, [(1, 1), (1, 1), (1, 1)], (1, 1, 1))
+        box_sets = [[stencil.inner_box(shape)], [b for b in list(slabs) + [interior]
+                                                 if all(h > l for l, h in zip(b[0], b[1]))]]
+        for v in range(len(stencil.variants())):
+            for r in (0, 1, 2, 3):
+                for boxes in box_sets:
+                    T2 = _nan_padded(shape, dtype, gpu, Tg)
+                    stencil.diffusion3d_(T2, Tn, Cpn, boxes=boxes, variant=v, rounds=r, **KW)
+                    torch.cuda.synchronize()
+                    got = T2.double().cpu()
+                    tol = 1e-12 if dtype == torch.float64 else 1e-5
+                    inner = (slice(1, -1),) * 3
+                    err = (got[inner] - ref[inner]).abs().max().item()
+                    if not err < tol:
+                        bad.append((shape, v, r, len(boxes), err))
+    assert not bad, bad[:10]
