@@ -348,6 +348,12 @@ PYBIND11_MODULE(_igg_native, m) {
            })
       .def("set_mode", [](HaloEngine& e, int m) { e.set_mode(static_cast<HaloMode>(m)); })
       .def_property_readonly("mode", [](HaloEngine& e) { return static_cast<int>(e.mode()); })
+      .def("set_pack_mode",
+           [](HaloEngine& e, int dim, int m) {
+             if (dim < 0 || dim >= NDIMS || m < 0 || m > 1) throw std::invalid_argument("set_pack_mode: bad dim/mode");
+             e.set_pack_mode(dim, static_cast<PackMode>(m));
+           })
+      .def("pack_mode", [](HaloEngine& e, int dim) { return static_cast<int>(e.pack_mode(dim)); })
       .def("resolved_mode", [](HaloEngine& e, const FieldSet& fs) {
         return static_cast<int>(e.resolved_mode(fs.f));
       })

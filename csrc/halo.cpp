@@ -257,9 +257,24 @@ void HaloEngine::exchange_dim_impl(const std::vector<Field>& fields, int dim, bo
   const bool has[2] = {left != PROC_NULL, right != PROC_NULL};
   if (!has[0] && !has[1]) return;
   const int eb = fields[0].elem_bytes;
+  const bool blit = device && pack_mode_[dim] == PackMode::Memcpy2D;
   auto do_copies = [&](const std::vector<Copy2D>& cps) {
     if (cps.empty()) return;
-    if (device) launch_copy2d(cps, eb, stream); else host_copy2d(cps, eb);
+    if (!device) return host_copy2d(cps, eb);
+    if (!blit) return launch_copy2d(cps, eb, stream);
+    std::vector<Copy2D> rest;
+    for (const Copy2D& c : cps) {
+      if (c.src_si != 1 || c.dst_si != 1) {
+        rest.push_back(c);
+        continue;
+      }
+      const size_t w = static_cast<size_t>(c.n_inner) * eb;
+      const size_t sp = c.n_outer > 1 ? static_cast<size_t>(c.src_so) * eb : w;
+      const size_t dp = c.n_outer > 1 ? static_cast<size_t>(c.dst_so) * eb : w;
+      IGG_HIP_CHECK(hipMemcpy2DAsync(c.dst, dp, c.src, sp, w, static_cast<size_t>(c.n_outer),
+                                     hipMemcpyDeviceToDevice, stream));
+    }
+    if (!rest.empty()) launch_copy2d(rest, eb, stream);
   };
 
   if (left == g.me && right == g.me) {

@@ -72,6 +72,15 @@ struct GridInfo {
 //   Auto:       OnePhase when a remote peer exists, else Sequential.
 enum class HaloMode : int { Sequential = 0, OnePhase = 1, Auto = 2 };
 
+// How the sequential schedule moves the strided faces of one dimension on the
+// GPU (the reference packs with write_d2x!/read_x2d! kernels and, for dims
+// 2/3 without GPU-aware MPI, with strided 3-D memcpys: src/update_halo.jl:
+// 432-465, 628-649).
+//   Kernel:   one batched copy2d launch for every face of every field.
+//   Memcpy2D: hipMemcpy2DAsync (SDMA/blit) per face whose rows are
+//             contiguous on both sides; other faces still use the kernel.
+enum class PackMode : int { Kernel = 0, Memcpy2D = 1 };
+
 // A face (one plane of a field orthogonal to `dim`) as a strided 2-D region.
 struct Face {
   char* base;
@@ -143,6 +152,8 @@ class HaloEngine {
   void exchange_dim(const std::vector<Field>& fields, int dim, hipStream_t stream);
   void set_mode(HaloMode m) { mode_ = m; }
   HaloMode mode() const { return mode_; }
+  void set_pack_mode(int dim, PackMode m) { pack_mode_.at(static_cast<size_t>(dim)) = m; }
+  PackMode pack_mode(int dim) const { return pack_mode_.at(static_cast<size_t>(dim)); }
   // Mode the next exchange of `fields` would use (Auto resolved).
   HaloMode resolved_mode(const std::vector<Field>& fields) const;
   int last_message_count() const { return last_msgs_; }
@@ -158,6 +169,7 @@ class HaloEngine {
   bool active(const Field& f, int d) const;
   GridInfo grid_;
   HaloMode mode_ = HaloMode::Auto;
+  std::array<PackMode, NDIMS> pack_mode_{PackMode::Kernel, PackMode::Kernel, PackMode::Kernel};
   int last_msgs_ = 0;
   BufferPool pool_;
   std::shared_ptr<Transport> host_transport_, dev_transport_;

@@ -125,11 +125,31 @@ def halo_mode() -> str:
     return {v: k for k, v in HALO_MODES.items()}[_engine.mode]
 
 
+def set_pack_mode(mode: str, dims=(True, True, True)) -> None:
+    """GPU face copies of the sequential schedule in the selected dims:
+    'kernel' (one batched copy launch per dim) or 'memcpy2d'
+    (hipMemcpy2DAsync per face with contiguous rows, the reference's strided
+    memcpy alternative; other faces keep the kernel). Also IGG_PACK[_DIMX/Y/Z]."""
+    _grid.check_initialized()
+    m = config.PACK_MODES.index(mode)
+    for d in range(NDIMS):
+        if dims[d]:
+            _engine.set_pack_mode(d, m)
+
+
+def pack_mode(dim: int) -> str:
+    """Pack mode of dimension ``dim`` (1-based, like the reference's dims)."""
+    _grid.check_initialized()
+    return config.PACK_MODES[_engine.pack_mode(dim - 1)]
+
+
 def _init_engine(gg) -> None:
     global _engine, _debug_sync
     _plans.clear()
     _engine = native.HaloEngine(_grid_info(gg))
     _engine.set_mode(HALO_MODES[config.halo_mode()])
+    for d, m in enumerate(config.pack_modes()):
+        _engine.set_pack_mode(d, config.PACK_MODES.index(m))
     _debug_sync = config.debug_sync()
     if gg.nprocs > 1:
         _engine.set_transport(gg.comm.host_transport(), False)

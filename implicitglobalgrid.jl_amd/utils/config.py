@@ -74,6 +74,25 @@ def halo_mode(env: Mapping[str, str] | None = None) -> str:
     return m
 
 
+PACK_MODES = ("kernel", "memcpy2d")
+
+
+def pack_modes(env: Mapping[str, str] | None = None) -> list[str]:
+    """``IGG_PACK`` sets all dims, ``IGG_PACK_DIMX/Y/Z`` override one dim:
+    ``kernel`` (default, batched copy kernel) | ``memcpy2d`` (hipMemcpy2DAsync
+    for faces with contiguous rows)."""
+    env = os.environ if env is None else env
+    modes = [env.get("IGG_PACK", "kernel").strip().lower()] * 3
+    for d, ax in enumerate("XYZ"):
+        k = f"IGG_PACK_DIM{ax}"
+        if k in env:
+            modes[d] = env[k].strip().lower()
+    for m in modes:
+        if m not in PACK_MODES:
+            raise ValueError(f"IGG_PACK / IGG_PACK_DIM*: expected kernel or memcpy2d (got {m!r})")
+    return modes
+
+
 def debug_sync(env: Mapping[str, str] | None = None) -> bool:
     env = os.environ if env is None else env
     return env.get("IGG_DEBUG_SYNC", "0") not in ("", "0")

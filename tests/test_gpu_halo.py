@@ -282,3 +282,53 @@ def test_gpu_debug_sync_phases(gpu, monkeypatch, transport):
         igg.update_halo_(Ag)
         assert torch.equal(Ag.cpu(), ref)
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32, torch.complex128])
+@pytest.mark.parametrize("loopback", [False, True])
+def test_gpu_pack_memcpy2d(gpu, dtype, loopback):
+    """IGG_PACK=memcpy2d (hipMemcpy2DAsync for faces with contiguous rows,
+    the kernel for the others) gives the same halos as the copy kernel:
+    self-periodic in-place path and the loopback pack -> transport -> unpack
+    path, sequential schedule, staggered fields in one call."""
+    from igg.parallel import halo as H
+
+    igg.init_global_grid(nx, ny, nz, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    if loopback:
+        H.enable_loopback()
+    H.set_halo_mode("sequential")
+    H.set_pack_mode("memcpy2d")
+    assert [H.pack_mode(d) for d in (1, 2, 3)] == ["memcpy2d"] * 3
+    cf = (1 + 1j) if dtype.is_complex else None
+    fs = [encode(torch.zeros(s, dtype=dtype), complex_factor=cf) for s in ((nx, ny, nz), (nx + 1, ny, nz),
+                                                                           (nx, ny, nz + 1))]
+    refs = [A.clone() for A in fs]
+    _check([zero_boundaries(A.clone()).to(gpu) for A in fs], refs, gpu)
+    H.set_pack_mode("kernel", dims=(False, True, False))
+    assert [H.pack_mode(d) for d in (1, 2, 3)] == ["memcpy2d", "kernel", "memcpy2d"]
+    _check([zero_boundaries(A.clone()).to(gpu) for A in fs], refs, gpu)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_gpu_pack_memcpy2d_in_graph(gpu):
+    """memcpy2d face copies are captured as graph memcpy nodes and replay."""
+    from igg.parallel import halo as H
+
+    igg.init_global_grid(16, 12, 10, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    H.set_pack_mode("memcpy2d")
+    A = encode(torch.zeros(16, 12, 10, dtype=torch.float64))
+    R = A.clone()
+    X = zero_boundaries(A.clone()).to(gpu)
+    igg.update_halo_(X)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        igg.update_halo_(X)
+    torch.cuda.synchronize()
+    H.register_graph(g)
+    X.copy_(zero_boundaries(A.clone()).to(gpu))
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(X.cpu(), R)
+    del g
+    igg.finalize_global_grid(finalize_MPI=False)

@@ -127,3 +127,28 @@ def test_env_flags_are_recorded(monkeypatch):
     assert gg.loopvectorization == [True, True, False]
     assert gg.cudaaware_MPI == [False, False, False]
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_pack_mode_env_parsing():
+    from igg.utils import config
+
+    assert config.pack_modes({}) == ["kernel"] * 3
+    assert config.pack_modes({"IGG_PACK": "memcpy2d"}) == ["memcpy2d"] * 3
+    assert config.pack_modes({"IGG_PACK": "memcpy2d", "IGG_PACK_DIMX": "kernel"}) == ["kernel", "memcpy2d", "memcpy2d"]
+    assert config.pack_modes({"IGG_PACK_DIMZ": "memcpy2d"}) == ["kernel", "kernel", "memcpy2d"]
+    with pytest.raises(ValueError):
+        config.pack_modes({"IGG_PACK": "dma"})
+
+
+def test_pack_mode_setter_cpu():
+    import torch
+
+    from igg.parallel import halo as H
+
+    igg.init_global_grid(6, 5, 4, quiet=True, init_MPI=False, device_type="none")
+    assert [H.pack_mode(d) for d in (1, 2, 3)] == ["kernel"] * 3
+    H.set_pack_mode("memcpy2d", dims=(False, True, True))
+    assert [H.pack_mode(d) for d in (1, 2, 3)] == ["kernel", "memcpy2d", "memcpy2d"]
+    A = torch.zeros(6, 5, 4)
+    igg.update_halo_(A)  # host fields ignore the device pack mode
+    igg.finalize_global_grid(finalize_MPI=False)
