@@ -28,6 +28,11 @@ from ..utils.tools import coords_g, nx_g, ny_g
 
 
 class Acoustic2D:
+    """2-D staggered acoustic wave propagation (pressure P at cell centres,
+    velocities Vx/Vy on staggered faces: nx+1 / ny+1) with one fused HIP kernel
+    per step and one ``update_halo_(Vx2, Vy2)`` (mixed overlaps); the 2-D
+    staggered config of BASELINE.json."""
+
     def __init__(self, *, dtype=torch.float32, device=None, K: float = 1.0, rho: float = 1.0,
                  lx: float = 10.0, ly: float = 10.0):
         gg = _grid.global_grid()

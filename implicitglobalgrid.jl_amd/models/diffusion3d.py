@@ -44,6 +44,13 @@ GRAPH_STEPS = 10
 
 
 class Diffusion3D:
+    """3-D heat diffusion with variable heat capacity on the local grid of the
+    implicit global grid (examples/diffusion3D_multigpu_CuArrays_novis.jl):
+    ``T2 = T + dt*lam/Cp * laplace(T)`` by one fused HIP kernel, then
+    ``update_halo_(T2)`` (or the fused exchange, ``set_fused``), ping-pong T/T2.
+    ``step``/``run`` advance, ``capture`` records hipGraphs, ``save``/``restore``
+    checkpoint."""
+
     def __init__(self, *, dtype=torch.float64, device=None, lam: float = 1.0, cp_min: float = 1.0,
                  lx: float = 10.0, ly: float = 10.0, lz: float = 10.0, overlap: bool = False,
                  slab_width=None, variant=None, halo_variant=None, interior_rounds: int = 0,

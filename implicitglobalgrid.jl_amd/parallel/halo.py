@@ -121,6 +121,7 @@ def set_halo_mode(mode: str) -> None:
 
 
 def halo_mode() -> str:
+    """The exchange schedule set by ``set_halo_mode`` / ``IGG_HALO_MODE``."""
     _grid.check_initialized()
     return {v: k for k, v in HALO_MODES.items()}[_engine.mode]
 
@@ -346,6 +347,8 @@ update_halo = update_halo_
 
 # --- ranges (update_halo.jl:544-563), 1-based like the reference --------------
 def sendranges(n: int, dim: int, A: torch.Tensor) -> list[range]:
+    """1-based index ranges of the plane of ``A`` sent to side ``n`` (1 left, 2 right) in ``dim``
+    (update_halo.jl:544-552)."""
     gg = _grid.global_grid()
     o = _ol(gg, dim - 1, A)
     if o < 2:
@@ -358,6 +361,8 @@ def sendranges(n: int, dim: int, A: torch.Tensor) -> list[range]:
 
 
 def recvranges(n: int, dim: int, A: torch.Tensor) -> list[range]:
+    """1-based index ranges of the halo plane of ``A`` received from side ``n`` in ``dim``
+    (update_halo.jl:555-563)."""
     gg = _grid.global_grid()
     if _ol(gg, dim - 1, A) < 2:
         raise IGGError("Incoherent arguments: ol(A,dim)<2.")
@@ -384,6 +389,7 @@ def allocate_bufs(*fields) -> None:
 
 
 def free_update_halo_buffers() -> None:
+    """Free the halo send/recv buffers (update_halo.jl:104-122); they are re-allocated on demand."""
     _release_graphs()
     if _engine is not None:
         native.device_synchronize() if _engine.pool_allocated(True) else None

@@ -25,11 +25,13 @@ def nx_g(A=None) -> int:
 
 
 def ny_g(A=None) -> int:
+    """Global grid size in y; with ``A``, the global size of array ``A`` (tools.jl:3-59)."""
     gg = _grid.global_grid()
     return int(gg.nxyz_g[1]) if A is None else int(gg.nxyz_g[1] + (_size(A, 1) - gg.nxyz[1]))
 
 
 def nz_g(A=None) -> int:
+    """Global grid size in z; with ``A``, the global size of array ``A`` (tools.jl:3-59)."""
     gg = _grid.global_grid()
     return int(gg.nxyz_g[2]) if A is None else int(gg.nxyz_g[2] + (_size(A, 2) - gg.nxyz[2]))
 
@@ -55,10 +57,12 @@ def x_g(ix: int, dx: float, A) -> float:
 
 
 def y_g(iy: int, dy: float, A) -> float:
+    """Global y-coordinate of element ``iy`` (1-based) of the local array ``A`` (tools.jl:146-155)."""
     return _coord(iy, dy, A, 1)
 
 
 def z_g(iz: int, dz: float, A) -> float:
+    """Global z-coordinate of element ``iz`` (1-based) of the local array ``A`` (tools.jl:194-203)."""
     return _coord(iz, dz, A, 2)
 
 

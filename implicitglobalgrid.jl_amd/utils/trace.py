@@ -19,11 +19,13 @@ from .._native import native
 
 
 def tracing() -> bool:
+    """Whether roctx ranges are emitted (IGG_TRACE / rocprofv3 marker tracing)."""
     return bool(native.trace_enabled())
 
 
 @contextlib.contextmanager
 def trace_range(name: str):
+    """Context manager: a named roctx range around a block (no-op when tracing is off)."""
     on = native.trace_enabled()
     if on:
         native.trace_push(name)

@@ -1,5 +1,7 @@
 """Port of test/test_tools.jl (exact vectors) and the x_g doctests
 (src/tools.jl:66-96), plus tic/toc."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -145,3 +147,14 @@ def test_coords_g_vectorised_matches_x_g_bitwise(per):
             ref = torch.tensor([f(i + 1, 0.37, A) for i in range(shape[dim])], dtype=torch.float64)
             assert torch.equal(v, ref)
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_api_docs_up_to_date():
+    """docs/api.md is generated from the docstrings (tools/gen_api_docs.py)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_api_docs.py"), "--check"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
