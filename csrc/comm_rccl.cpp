@@ -1,4 +1,5 @@
 // RCCL transport (see include/igg/comm.hpp).
+#include <cstdlib>
 #include <cstring>
 
 #include <hip/hip_runtime_api.h>
@@ -31,7 +32,19 @@ RcclComm::RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank)
   if (uid.size() != sizeof(ncclUniqueId)) fail("RcclComm: bad unique id size ", uid.size());
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
-  IGG_NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+  // IGG_RCCL_MAX_CTAS caps the workgroups (channels) of RCCL's kernels, which
+  // otherwise take CUs from a concurrently running interior stencil in the
+  // overlapped step (RCCL interplay). Unset = RCCL's default.
+  const char* env = std::getenv("IGG_RCCL_MAX_CTAS");
+  const int max_ctas = env ? std::atoi(env) : 0;
+  if (max_ctas > 0) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.minCTAs = 1;
+    cfg.maxCTAs = max_ctas;
+    IGG_NCCL_CHECK(ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg));
+  } else {
+    IGG_NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+  }
   IGG_HIP_CHECK(hipMalloc(&scratch_, 256));
   IGG_HIP_CHECK(hipMemset(scratch_, 0, 256));
   IGG_HIP_CHECK(hipDeviceSynchronize());

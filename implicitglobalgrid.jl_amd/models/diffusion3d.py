@@ -301,6 +301,15 @@ class Diffusion3D:
             raise ValueError("Diffusion3D.capture: steps must be even and >= 2")
         if self.device.type != "cuda":
             raise RuntimeError("Diffusion3D.capture: hipGraphs need a GPU model")
+        if self.overlap and not self.fused:
+            from ..parallel import halo as H
+
+            if H.transport_name() == "rccl":
+                # Capturing RCCL on the forked halo stream of the overlapped
+                # step crashed the process in RCCL 2.26 (profiles/r1_ctas/):
+                # refuse loudly; run() then steps eagerly.
+                raise RuntimeError("Diffusion3D.capture: the overlapped step with the RCCL transport "
+                                   "cannot be captured; use the serial step, the put transport or eager steps")
         if not self._warm:
             self.step()
         if self.fused and not self._fprimed:
