@@ -30,6 +30,7 @@ SECTIONS = [
     ("Applications", "igg.models.diffusion3d", ["Diffusion3D"]),
     ("", "igg.models.acoustic2d", ["Acoustic2D"]),
     ("Tracing", "igg.utils.trace", None),
+    ("Launcher", "igg.utils.launch", ["launch", "main"]),
 ]
 
 
