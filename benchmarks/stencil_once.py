@@ -15,6 +15,8 @@ ap.add_argument("--n", type=int, default=512)
 ap.add_argument("--variants", default="0")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--dtype", default="float64")
+ap.add_argument("--rounds", default="0", help="grid residency rounds per launch (list; 0 = default)")
+ap.add_argument("--calib", action="store_true", help="also run T2.copy_(T) (known bytes) for counter calibration")
 a = ap.parse_args()
 dt = getattr(torch, a.dtype)
 n = a.n
@@ -23,8 +25,12 @@ Cp = 1 + torch.rand((n, n, n), dtype=dt, device="cuda")
 T2 = T.clone()
 s = torch.cuda.current_stream().cuda_stream
 for v in [int(x) for x in a.variants.split(",")]:
+    for gr in [int(x) for x in a.rounds.split(",")]:
+        for _ in range(a.reps):
+            native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], [1.0, 1.0, 1.0], 0.01,
+                               T.element_size(), [((1, 1, 1), (n - 1, n - 1, n - 1))], True, v, s, gr)
+if a.calib:
     for _ in range(a.reps):
-        native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], [1.0, 1.0, 1.0], 0.01,
-                           T.element_size(), [((1, 1, 1), (n - 1, n - 1, n - 1))], True, v, s)
+        T2.copy_(T)  # reads n^3 and writes n^3 elements
 torch.cuda.synchronize()
 print("done")
