@@ -1,4 +1,7 @@
 // RCCL transport (see include/igg/comm.hpp).
+// Replaces the reference's per-(side, field) MPI.Irecv!/Isend with tag 0
+// (update_halo.jl:713-735) by one ncclGroupStart/End of raw-byte ncclSend/ncclRecv
+// per exchange phase on the halo stream.
 #include <cstdlib>
 #include <cstring>
 

@@ -1,3 +1,7 @@
+// FusedHalo: arena regions and neighbour sync for the stencil kernel that stores its
+// send planes straight into the neighbours' arenas. Produces the halos that
+// update_halo!(T) (examples/diffusion3D_multigpu_CuArrays_novis.jl:47, update_halo.jl:32-78)
+// would, without a separate pack/send/unpack pass.
 #include "igg/fused.hpp"
 
 #include <algorithm>

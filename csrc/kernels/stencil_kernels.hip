@@ -1,4 +1,6 @@
 // Fused 3-D heat-diffusion stencil for gfx950 (CDNA4).
+// Computes the update of examples/diffusion3D_multigpu_CuArrays_novis.jl:42-46
+// (five broadcasts and four temporaries there) in one kernel.
 //
 // Regime: 7-point update, ~15 flop per cell against >= 24 B (f64) of compulsory
 // HBM traffic -> < 1 flop/B: HBM-bandwidth bound, so MFMA buys nothing here

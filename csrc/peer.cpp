@@ -1,3 +1,6 @@
+// PeerMesh: IPC-mapped peer arenas and epoch flags of the one-sided "put" transport.
+// MI355X-specific replacement of the reference's MPI point-to-point layer
+// (update_halo.jl:713-753); no counterpart exists in the reference.
 #include "igg/peer.hpp"
 
 #include "igg/ipc.hpp"

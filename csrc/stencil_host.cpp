@@ -1,4 +1,6 @@
 // Host (CPU) diffusion step and the boundary/interior box decomposition.
+// Same update as examples/diffusion3D_multicpu_novis.jl:42-46 (qx/qy/qz, dTedt,
+// T interior), evaluated in one pass without the flux temporaries.
 #include <algorithm>
 
 #include "igg/copy.hpp"

@@ -1,4 +1,7 @@
 // Cartesian topology math (see include/igg/topology.hpp).
+// Reference behaviour: init_global_grid.jl:84-93 (MPI.Dims_create!, Cart_create,
+// Cart_coords, Cart_shift and nxyz_g = dims.*(nxyz.-overlaps) .+ overlaps.*(periods.==0)).
+// No MPI here: balanced dims, row-major coords and shifts are computed directly.
 #include "igg/topology.hpp"
 
 #include <algorithm>

@@ -1,3 +1,5 @@
+// roctx ranges (loaded with dlopen, no link-time dependency). The reference has no
+// tracing beyond tic/toc (tools.jl:205-236); see SURVEY.md §5.1.
 #include "igg/trace.hpp"
 
 #include <dlfcn.h>
