@@ -39,7 +39,12 @@ import time
 
 # Fused-halo kernel candidates of the A/B: (tiling variant, send mode, grid
 # residency rounds) - the front of benchmarks/fused_sweep.py --grid on MI355X.
-FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3))
+# Modes 2/3 = 0/1 with the z-edge exchange compiled out when there is no z
+# neighbour (2x1x1, 2x2x1): that form of tiling 11 (the fastest plain tiling,
+# which pays for the z exchange at its register cliff) is tried as well
+# (profiles/r1_noz/: loopback 2x2x1 rank 0.632 vs 0.651 ms/step).
+FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3),
+                    (11, 2, 2), (11, 3, 2))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
@@ -71,6 +76,9 @@ def parse():
                     help="force the boundary/interior split with the halo on a second stream (default: A/B decides)")
     ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
     ap.add_argument("--periodic", action="store_true", help="periodic boundaries in every dim")
+    ap.add_argument("--periodic-dims", default=None,
+                    help="periodic boundaries in a subset of 'xyz' only (with --loopback, 'xy' emulates "
+                         "an interior rank of a 2x2x1 topology: no z exchange)")
     ap.add_argument("--loopback", action="store_true",
                     help="1 GPU: route all 6 faces through the RCCL remote path to itself (interior-rank emulation)")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
@@ -237,19 +245,23 @@ def main():
     n = args.n or cfg["n"]
     gather_every = cfg["gather_every"] if args.gather_every is None else args.gather_every
     is2d = cfg["model"] == "acoustic2d"
-    per = 1 if args.periodic else 0
+    pdims = "xyz" if args.periodic else (args.periodic_dims or "")
+    if set(pdims) - set("xyz"):
+        raise SystemExit(f"--periodic-dims: expected a subset of 'xyz', got {pdims!r}")
+    perx, pery, perz = (int(c in pdims) for c in "xyz")
     if args.transport != "auto":
         os.environ["IGG_TRANSPORT"] = args.transport
     # A put exchange that cannot complete must not stall the run for long.
     os.environ.setdefault("IGG_PUT_TIMEOUT", "20")
     if args.share_gpu:
         os.environ.setdefault("IGG_TRANSPORT", "staged")
-    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, 1 if is2d else n, periodx=per, periody=per,
-                                                         periodz=0 if is2d else per, quiet=True,
+    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, 1 if is2d else n, periodx=perx, periody=pery,
+                                                         periodz=0 if is2d else perz, quiet=True,
                                                          select_device=not args.share_gpu)
     log = (lambda m: print(m, file=sys.stderr, flush=True)) if me == 0 else (lambda m: None)
     if args.loopback:
-        H.enable_loopback((True, True, not is2d))
+        lb = (bool(perx), bool(pery), bool(perz)) if pdims else (True, True, True)
+        H.enable_loopback((lb[0], lb[1], lb[2] and not is2d))
     model = Acoustic2D(dtype=dtype) if is2d else Diffusion3D(dtype=dtype, overlap=args.overlap)
     field = (lambda: model.P) if is2d else (lambda: model.T)
     A_global = None
@@ -261,7 +273,7 @@ def main():
     if nprocs > 1 and args.transport == "auto" and not args.overlap:
         _, ab = select_transport(model, field(), comm, log, ref="staged" if args.share_gpu else "rccl")
     fused_ab = None
-    if not is2d and not args.overlap and (nprocs > 1 or args.loopback or args.periodic):
+    if not is2d and not args.overlap and (nprocs > 1 or args.loopback or pdims):
         fused_ab = select_fused(model, comm, log, args.fused)
     for _ in range(args.warmup):
         model.step()

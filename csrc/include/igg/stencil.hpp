@@ -62,7 +62,8 @@ bool diffusion3d_fused_variant_ok(int v);
 // Inner-box update through the fused kernel without exchange features
 // (tiling = a fused-capable variant index); used by the "hx" variants.
 void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t stream);
-// mode 0: sends stored as computed; 1: deferred one x step (see fused_kernels.hip).
+// mode 0: sends stored as computed; 1: deferred one x step; + 2: z-edge exchange
+// compiled out when there is no z neighbour (see fused_kernels.hip).
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
                               hipStream_t stream);
 void host_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes);

@@ -346,10 +346,26 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
 // 1 = deferred by one x step (their acknowledgement latency over xGMI can
 // never gate the next step's loads). The z edge is lane-distributed in both
 // (a per-row direct variant measured 5-100 us slower: profiles/fused/).
+//
+// Mode bit 2 (modes 2/3 = 0/1 + 2): without a z neighbour (dims[2] == 1 and
+// not periodic: the 2x1x1 and 2x2x1 topologies of 2 and 4 ranks) the z-edge
+// exchange is compiled out (FEAT 195 = x/y in/out). Results are identical (207
+// skips the null z sides at run time). It pays for the 255-VGPR tiling 11
+// (loopback 2x2x1 interior rank: 0.632 vs 0.651 ms for the best 207 form) but
+// the other tilings' 195 forms measured slower than their 207 forms
+// (profiles/r1_noz/), so it is an A/B choice, not automatic.
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ>
 void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStream_t s) {
-  if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false>(d, io, s);
-  else launch_hx<T, BY, RY, VZ, PF, BZ, true>(d, io, s);
+  const bool zx = io.in[2][0] || io.in[2][1] || io.out[2][0] || io.out[2][1];
+  if (zx || !(mode & 2)) {
+    mode &= 1;
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207>(d, io, s);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207>(d, io, s);
+  } else {
+    mode &= 1;
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195>(d, io, s);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195>(d, io, s);
+  }
 }
 
 template <typename T>
@@ -407,7 +423,7 @@ bool diffusion3d_fused_variant_ok(int v) {
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
                               hipStream_t stream) {
   if (a.n[0] < 3 || a.n[1] < 3 || a.n[2] < 3) fail("diffusion3d: every extent must be >= 3");
-  if (mode != 0 && mode != 1) fail("diffusion3d (fused halo): mode must be 0 or 1");
+  if (mode < 0 || mode > 3) fail("diffusion3d (fused halo): mode must be 0..3");
   if (a.elem_bytes == 8) dispatch<double>(a, io, variant, mode, stream);
   else if (a.elem_bytes == 4) dispatch<float>(a, io, variant, mode, stream);
   else fail("diffusion3d: only float32/float64 are supported");

@@ -73,6 +73,25 @@ def test_fused_partial_periodic(gpu, periods):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("variant", [0, 2, 9, 11, 14])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("periods", [(1, 1, 0), (1, 1, 1)])
+def test_fused_no_z_exchange_matches_update_halo(gpu, variant, dtype, mode, periods):
+    """Modes 2/3: with x/y neighbours only (a 2x2x1 rank) the kernel form without
+    the z-edge exchange (FEAT 195 in fused_kernels.hip) runs, for every tiling,
+    send mode and dtype; with a z neighbour they fall back to the full form."""
+    a, b = _pair((34, 29, 136), periods, dtype, variant, mode=mode)
+    a.run(7)
+    b.run(7)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
 def test_fused_loopback_graph_and_mode_switches(gpu):
     """Loopback grid, hipGraph replays with odd/even step counts, sync_halo in
     between (re-primes from the field) and switching back to update_halo_."""
