@@ -126,7 +126,8 @@ class Diffusion3D:
         # half parity), whether the arena holds the halos of the current T.
         self.fused = False
         # Fused kernel: variant (tiling; one with a fused instantiation) and
-        # send mode (0 stores as computed, 1 deferred one x step).
+        # send mode (0 stores as computed, 1 deferred one x step; +2 compiles the
+        # z-edge exchange out when there is no z neighbour).
         self.fused_variant = 0
         self.fused_mode = 0
         self.fused_rounds = 3  # grid residency rounds (profiles/r1_fused/grid.log)
