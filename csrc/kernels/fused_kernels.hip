@@ -60,8 +60,10 @@ struct HxScal {
 };
 
 // FEAT bits (compile-time exchange features): 1 x-in, 2 y-in, 4 z-in, 8 z-out,
-// 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants). 207 = the full exchange, 0 = the plain update (variants
-// 21+); other subsets served the cost bisect (profiles/r1_fused/feature_bisect_*).
+// 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants); 512 =
+// lane-distributed z-segment edge loads (plain variants, below). 207 = the full
+// exchange, 0 = the plain update (variants 21+); other subsets served the cost
+// bisect (profiles/r1_fused/feature_bisect_*).
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
 __global__ void __launch_bounds__(64 * BY * BZ)
 diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
@@ -106,6 +108,15 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   const bool load_next = lane == 63 || z0 + VZ > zhi_v;
   const int zpi = static_cast<int>(max<int64_t>(zc - 1, 0) - zt);
   const int zni = static_cast<int>(min<int64_t>(zc + VZ, n2 - 1) - zt);
+  // FEAT 512: the z neighbours across the segment's ends (lane 0's prev, the
+  // load_next lanes' next: one uniform element per row each) are fetched by
+  // lanes r / 32+r with ONE load per x step, one step ahead, and moved with
+  // readlane - instead of 2*RY single-lane loads held in 2*RY registers.
+  static_assert(!(FEAT & 512) || RY <= 32, "FEAT 512: at most 32 rows per wave");
+  const int64_t zc63 = min<int64_t>(zt + 63 * VZ, zhi_v);
+  const int zedge = lane < 32 ? static_cast<int>(max<int64_t>(zt - 1, 0) - zt)
+                              : static_cast<int>(min<int64_t>(zc63 + VZ, n2 - 1) - zt);
+  const int64_t rowe = (y0 + min(lane & 31, nv - 1)) * n2 + zt + zedge;
 
   int64_t rowb[RY];
 #pragma unroll
@@ -167,8 +178,15 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     cp[r] = ldc(cpp + xs * s0 + rowb[r] + zl);
   }
   const T two = T(2);
+  T evn = T(0);
+  if constexpr ((FEAT & 512) != 0) evn = t[xs * s0 + rowe];
   for (int64_t x = xs; x < xe; ++x) {
     const int64_t off = x * s0;
+    T evc = T(0);
+    if constexpr ((FEAT & 512) != 0) {
+      evc = evn;
+      if (x + 1 < xe) evn = t[off + s0 + rowe];
+    }
     // z halo of plane x (fetched one step ahead), prefetch plane x+1's. (The
     // alternative of substituting it at its use measured slower for every
     // tiling: profiles/r1_fused/feature_bisect_v11_zin_alt.log.)
@@ -202,10 +220,12 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     const V ym = vld<T, VZ>(ymb + x * yms + zl);
     const V yp = vld<T, VZ>(ypb + x * yps + zl);
     T em[RY], ep[RY];
+    if constexpr ((FEAT & 512) == 0) {
 #pragma unroll
-    for (int r = 0; r < RY; ++r) {
-      em[r] = load_prev ? t[off + rowb[r] + zpi] : T(0);
-      ep[r] = load_next ? t[off + rowb[r] + zni] : T(0);
+      for (int r = 0; r < RY; ++r) {
+        em[r] = load_prev ? t[off + rowb[r] + zpi] : T(0);
+        ep[r] = load_next ? t[off + rowb[r] + zni] : T(0);
+      }
     }
     if constexpr (DF) {
       if (ysend_dst) *reinterpret_cast<V*>(ysend_dst) = ysend;
@@ -220,8 +240,14 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
       const V& yn = (r + 1 < nv) ? tc[(r + 1 < RY) ? r + 1 : r] : yp;
       T prev = __shfl_up(c[VZ - 1], 1);
       T next = __shfl_down(c[0], 1);
-      if (load_prev) prev = em[r];
-      if (load_next) next = ep[r];
+      if constexpr ((FEAT & 512) != 0) {
+        const T pv = lane_read(evc, r), nx = lane_read(evc, 32 + r);
+        if (load_prev) prev = pv;
+        if (load_next) next = nx;
+      } else {
+        if (load_prev) prev = em[r];
+        if (load_next) next = ep[r];
+      }
       V out;
 #pragma unroll
       for (int e = 0; e < VZ; ++e) {
@@ -295,14 +321,14 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   if (remote) __builtin_amdgcn_s_waitcnt(0);
 }
 
-int resident(const void* kernel, int block) {
+int resident(const void* kernel, int block, size_t lds = 0) {
   static std::vector<std::pair<const void*, int>> cache;
   for (const auto& c : cache)
     if (c.first == kernel) return c.second;
   int dev = 0, cus = 0, occ = 0;
   IGG_HIP_CHECK(hipGetDevice(&dev));
   IGG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  IGG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, 0));
+  IGG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, lds));
   const int r = std::max(1, occ) * std::max(1, cus);
   cache.emplace_back(kernel, r);
   return r;
@@ -322,7 +348,10 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
   a.nty = (n1 - 2 + TY - 1) / TY;
   const int64_t len0 = n0 - 2, tiles = a.ntz * a.nty;
   const int rounds = d.rounds > 0 ? d.rounds : 1;
-  const int64_t target = static_cast<int64_t>(rounds) * resident(reinterpret_cast<const void*>(kern), block);
+  // FEAT 1024: one workgroup per CU, enforced with an unused dynamic LDS
+  // allocation (isolates the occupancy effect of the lower-VGPR FEAT 512 form).
+  const size_t lds = (FEAT & 1024) ? 96 * 1024 : 0;
+  const int64_t target = static_cast<int64_t>(rounds) * resident(reinterpret_cast<const void*>(kern), block, lds);
   const int64_t ch_all = std::max<int64_t>(1, (len0 * tiles + target - 1) / target);
   const int64_t nch = std::max<int64_t>(1, (len0 + ch_all - 1) / ch_all);
   a.ch = (len0 + nch - 1) / nch;
@@ -334,7 +363,7 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
   a.dtlam = static_cast<T>(d.dt_lam);
   auto in = [&](int k, int s) { return reinterpret_cast<const T*>(io.in[k][s]); };
   auto out = [&](int k, int s) { return reinterpret_cast<T*>(io.out[k][s]); };
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(block), 0, stream,
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(block), lds, stream,
                      reinterpret_cast<T*>(d.t2), reinterpret_cast<const T*>(d.t), reinterpret_cast<const T*>(d.cp),
                      in(0, 0), in(0, 1), in(1, 0), in(1, 1), in(2, 0), in(2, 1), out(0, 0), out(0, 1), out(1, 0),
                      out(1, 1), out(2, 0), out(2, 1), a);
@@ -403,6 +432,11 @@ void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
     case 111: launch_hx<T, 4, 4, 4, false, 1, false, 256>(d, none, s); break;
     case 112: launch_hx<T, 4, 8, 4, false, 1, false, 256>(d, none, s); break;
     case 113: launch_hx<T, 2, 8, 4, false, 2, false, 256>(d, none, s); break;
+    case 120: launch_hx<T, 4, 8, 2, false, 1, false, 512>(d, none, s); break;  // + lane-distributed z edges
+    case 121: launch_hx<T, 4, 8, 4, false, 1, false, 512>(d, none, s); break;
+    case 122: launch_hx<T, 2, 8, 2, false, 1, false, 512>(d, none, s); break;
+    case 123: launch_hx<T, 4, 4, 4, false, 1, false, 512>(d, none, s); break;
+    case 124: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024>(d, none, s); break;
     default: fail("diffusion3d (restrict form): tiling ", v, " not instantiated");
   }
 }

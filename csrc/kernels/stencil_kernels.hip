@@ -323,11 +323,17 @@ constexpr Variant VARIANTS[] = {
     {"hx_v4_by4_ry4_nt_ntc", 4, 4, 4, false, true},     // 33
     {"hx_v4_by4_ry8_nt_ntc", 4, 8, 4, false, true},     // 34
     {"hx_v4_bz2_by2_ry8_nt_ntc", 2, 8, 4, false, true}, // 35
+    // 36-39: restrict form with lane-distributed z-segment edge loads (tilings of 11, 9, 26, 0)
+    {"hx_v2_by4_ry8_nt_zl", 4, 8, 2, false, true},      // 36
+    {"hx_v4_by4_ry8_nt_zl", 4, 8, 4, false, true},      // 37
+    {"hx_v2_by2_ry8_nt_zl", 2, 8, 2, false, true},      // 38
+    {"hx_v4_by4_ry4_nt_zl", 4, 4, 4, false, true},      // 39
+    {"hx_v2_by4_ry8_nt_zl_occ1", 4, 8, 2, false, true}, // 40 (one workgroup per CU)
 };
 // Variants 21..31: restrict-form tiling id (fused_kernels.hip dispatch_plain)
 // and the stencil_kernels.hip variant used for boxes other than the inner box.
-constexpr int HX_TILING[] = {0, 2, 9, 11, 14, 100, 101, 102, 103, 104, 105, 110, 111, 112, 113};
-constexpr int HX_FALLBACK[] = {0, 2, 9, 11, 14, 11, 11, 11, 2, 5, 11, 11, 0, 9, 14};
+constexpr int HX_TILING[] = {0, 2, 9, 11, 14, 100, 101, 102, 103, 104, 105, 110, 111, 112, 113, 120, 121, 122, 123, 124};
+constexpr int HX_FALLBACK[] = {0, 2, 9, 11, 14, 11, 11, 11, 2, 5, 11, 11, 0, 9, 14, 11, 9, 11, 0, 11};
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
 // Grid sizing policy: `g_rounds` full residency rounds (resident workgroups =

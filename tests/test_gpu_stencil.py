@@ -70,12 +70,13 @@ def test_variant_float32(gpu, variant):
 
 
 @pytest.mark.parametrize("hx,tiling", [(21, 0), (22, 2), (23, 9), (24, 11), (25, 14), (32, 11), (33, 0), (34, 9),
-                                       (35, 14)])
+                                       (35, 14), (36, 11), (37, 9), (38, 26), (39, 0), (40, 11)])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_restrict_form_bitwise_equals_vkernel(gpu, hx, tiling, dtype):
     """Variants 21-25 (inner box through fused_kernels.hip without exchange
     features) compute exactly what the stencil_kernels.hip variant with the
-    same tiling computes."""
+    same tiling computes; 32-39 (non-temporal Cp, lane-distributed z-segment
+    edges) exactly what the plain restrict form computes."""
     shape = (26, 35, 136)
     _, _, Tg, Cpg = _fields(shape, dtype, gpu)
     a = torch.zeros_like(Tg)
