@@ -43,6 +43,9 @@ import time
 # neighbour (2x1x1, 2x2x1): that form of tiling 11 (the fastest plain tiling,
 # which pays for the z exchange at its register cliff) is tried as well
 # (profiles/r1_noz/: loopback 2x2x1 rank 0.632 vs 0.651 ms/step).
+# (Fused variant 40 - tiling 11 with lane-distributed z-segment edge loads at
+# one workgroup per CU, no register spill - measured 0.65-0.75 ms in every
+# loopback topology, slower than these: profiles/r1_zl/.)
 FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3),
                     (11, 2, 2), (11, 3, 2))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU

@@ -383,17 +383,18 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
 // (loopback 2x2x1 interior rank: 0.632 vs 0.651 ms for the best 207 form) but
 // the other tilings' 195 forms measured slower than their 207 forms
 // (profiles/r1_noz/), so it is an A/B choice, not automatic.
-template <typename T, int BY, int RY, int VZ, bool PF, int BZ>
+// XF: extra FEAT bits of the tiling (512 | 1024 for fused variant 40).
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, int XF = 0>
 void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStream_t s) {
   const bool zx = io.in[2][0] || io.in[2][1] || io.out[2][0] || io.out[2][1];
   if (zx || !(mode & 2)) {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207>(d, io, s);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207>(d, io, s);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s);
   } else {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195>(d, io, s);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195>(d, io, s);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF>(d, io, s);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF>(d, io, s);
   }
 }
 
@@ -405,6 +406,7 @@ void dispatch(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hip
     case 9: launch_mode<T, 4, 8, 4, false, 1>(d, io, mode, s); break;
     case 11: launch_mode<T, 4, 8, 2, false, 1>(d, io, mode, s); break;
     case 14: launch_mode<T, 2, 8, 4, false, 2>(d, io, mode, s); break;
+    case 40: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024>(d, io, mode, s); break;
     default: fail("diffusion3d (fused halo): variant ", v, " has no fused instantiation");
   }
 }
@@ -437,6 +439,8 @@ void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
     case 122: launch_hx<T, 2, 8, 2, false, 1, false, 512>(d, none, s); break;
     case 123: launch_hx<T, 4, 4, 4, false, 1, false, 512>(d, none, s); break;
     case 124: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024>(d, none, s); break;
+    case 125: launch_hx<T, 4, 10, 2, false, 1, false, 512 | 1024>(d, none, s); break;
+    case 126: launch_hx<T, 4, 12, 2, false, 1, false, 512 | 1024>(d, none, s); break;
     default: fail("diffusion3d (restrict form): tiling ", v, " not instantiated");
   }
 }
@@ -451,7 +455,7 @@ void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t
 }
 
 bool diffusion3d_fused_variant_ok(int v) {
-  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14;
+  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14 || v == 40;
 }
 
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
