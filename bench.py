@@ -47,7 +47,7 @@ import time
 # one workgroup per CU, no register spill - measured 0.65-0.75 ms in every
 # loopback topology, slower than these: profiles/r1_zl/.)
 FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3),
-                    (11, 2, 2), (11, 3, 2))
+                    (11, 2, 2), (11, 3, 2), (50, 0, 2), (50, 1, 2), (50, 1, 4))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")

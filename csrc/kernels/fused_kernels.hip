@@ -407,6 +407,7 @@ void dispatch(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hip
     case 11: launch_mode<T, 4, 8, 2, false, 1>(d, io, mode, s); break;
     case 14: launch_mode<T, 2, 8, 4, false, 2>(d, io, mode, s); break;
     case 40: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024>(d, io, mode, s); break;
+    case 50: launch_mode<T, 4, 4, 4, false, 1, 1024>(d, io, mode, s); break;  // tiling 0, one WG per CU
     default: fail("diffusion3d (fused halo): variant ", v, " has no fused instantiation");
   }
 }
@@ -455,7 +456,7 @@ void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t
 }
 
 bool diffusion3d_fused_variant_ok(int v) {
-  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14 || v == 40;
+  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14 || v == 40 || v == 50;
 }
 
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
