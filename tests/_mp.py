@@ -8,6 +8,8 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -18,9 +20,20 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def run_ranks(nprocs: int, scenario: str, *args, timeout: float = 240.0, env_extra=None) -> list[str]:
+# Every multi-rank test ends within this many seconds: below the GPU box's
+# 180 s no-output limit, so a hang fails its test (with every rank's output)
+# instead of getting the whole run killed silently.
+MAX_TIMEOUT = 170.0
+
+
+def run_ranks(nprocs: int, scenario: str, *args, timeout: float = 150.0, env_extra=None) -> list[str]:
+    """Run ``scenario`` on ``nprocs`` ranks. Fail-fast: the first rank that
+    exits non-zero stops the others (a dead rank would otherwise leave its
+    peers blocked in a collective until the timeout); on a timeout every
+    rank's output tail is reported."""
+    timeout = min(timeout, MAX_TIMEOUT)
     port = free_port()
-    procs = []
+    procs, logs = [], []
     for r in range(nprocs):
         env = dict(os.environ)
         env.update({
@@ -30,21 +43,39 @@ def run_ranks(nprocs: int, scenario: str, *args, timeout: float = 240.0, env_ext
         })
         if env_extra:
             env.update(env_extra)
+        log = tempfile.TemporaryFile(mode="w+")
+        logs.append(log)
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), scenario, *map(str, args)],
-            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, cwd=ROOT))
-    outs, failed = [], []
-    for r, p in enumerate(procs):
-        try:
-            out, _ = p.communicate(timeout=timeout)
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
-            raise AssertionError(f"rank {r} timed out in scenario {scenario}")
-        outs.append(out)
-        if p.returncode != 0:
-            failed.append((r, p.returncode, out[-4000:]))
-    if failed:
-        msg = "\n".join(f"--- rank {r} rc={rc}\n{o}" for r, rc, o in failed)
-        raise AssertionError(f"scenario {scenario} failed:\n{msg}")
+            env=env, stdout=log, stderr=subprocess.STDOUT, text=True, cwd=ROOT))
+    deadline = time.monotonic() + timeout
+    first_bad = None
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [r for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                first_bad = bad[0]
+                break
+            if all(c == 0 for c in codes) or time.monotonic() > deadline:
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            p.wait()
+    outs = []
+    for log in logs:
+        log.seek(0)
+        outs.append(log.read())
+        log.close()
+    codes = [p.returncode for p in procs]
+    if first_bad is not None:
+        raise AssertionError(f"scenario {scenario}: rank {first_bad} failed (rc={codes[first_bad]}), "
+                             f"the others were stopped:\n{outs[first_bad][-4000:]}")
+    if any(c != 0 for c in codes):
+        msg = "\n".join(f"--- rank {r} rc={c}\n{o[-1500:]}" for r, (c, o) in enumerate(zip(codes, outs)))
+        raise AssertionError(f"scenario {scenario} timed out after {timeout:.0f} s:\n{msg}")
     return outs

@@ -98,7 +98,7 @@ def test_put_transport_timeout_reports_and_never_hangs():
 
 @pytest.mark.gpu
 def test_put_transport_absorbs_rank_skew():
-    run_ranks(4, "put_skew", 12, env_extra=PUT_ENV, timeout=200)
+    run_ranks(4, "put_skew", 12, env_extra=PUT_ENV, timeout=170)
 
 
 @pytest.mark.gpu
@@ -116,7 +116,7 @@ def test_gather_async_gpu(nprocs):
 def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
     # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
-    run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=200)
+    run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=170)
 
 
 @pytest.mark.gpu
@@ -125,4 +125,4 @@ def test_fused_soak_with_rank_skew(nprocs, kernel):
     """Thousands of graph-replayed fused steps with random host skew between
     ranks stay bitwise equal to stencil + update_halo_."""
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "30", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
-    run_ranks(nprocs, "fused_soak", 20, 18, 32, 60, 40, env_extra=env, timeout=300)
+    run_ranks(nprocs, "fused_soak", 20, 18, 32, 60, 40, env_extra=env, timeout=170)
