@@ -4,30 +4,38 @@
 Metric (BASELINE.json): effective memory throughput T_eff = A_eff / t_it with
 A_eff = 3 * n_local * sizeof(T) (T read, Cp read, T2 written) per GPU, and the
 weak-scaling efficiency E(N) = t_it(1)/t_it(N) (computed by the driver from the
-per-N values). ``value`` is the WHOLE-JOB aggregate T_eff (sum over GPUs).
-``vs_baseline`` compares the per-GPU T_eff with the reference's derived
-23 GB/s per GPU (8x P100, 256^3/GPU diffusion example).
+per-N values).
 
-One process per GPU (torchrun); each rank owns a 512^3 block; the process
-topology comes from init_global_grid (2 GPUs -> 2x1x1, 4 -> 2x2x1,
-8 -> 2x2x2); every step = fused stencil + halo exchange: update_halo_ after
-the stencil, or the fused exchange from inside the stencil kernel (below).
+``value`` is the WHOLE-JOB aggregate T_eff (sum of the per-GPU T_eff over the
+N GPUs), as the bench contract prescribes; at N=1 it equals the per-GPU number.
+The per-GPU T_eff is ``config.t_eff_per_gpu_GBs`` (``value / n_gpus``), the
+per-step time ``ms_per_step`` (= ``config.t_it_ms``). ``vs_baseline`` compares
+the per-GPU T_eff with the reference's derived 23 GB/s per GPU (BASELINE.md:
+8x P100, 256^3/GPU diffusion example), like for like.
 
-Multi-GPU: ``--transport auto`` (default) checks that the one-sided put
-transport reproduces the RCCL exchange bitwise on this node, times a few steps
-with each (MAX over ranks) during warm-up and keeps the faster; the timed
-steps are replayed from a hipGraph (GRAPH_STEPS=10 steps per replay) unless
---no-graph.
+Launch: one process per GPU. Under torchrun (``WORLD_SIZE`` set) every rank
+runs this file. ``python bench.py --gpus N`` WITHOUT a launcher starts the N
+ranks itself (``self_launch``: a parent that never touches the GPU spawns N
+single-GPU children with the torch.distributed environment, prints rank 0's
+JSON line, and fails if any rank fails or ``n_gpus != N``); a ``--gpus`` that
+contradicts ``WORLD_SIZE`` is an error, never a silent 1-GPU number.
+(Reference: nprocs comes from the communicator, src/init_global_grid.jl:84-93.)
 
-``--fused auto`` (default; diffusion3d with neighbours): the stencil kernel
-itself stores its send planes into the neighbours' IPC-mapped arenas over xGMI
-and a 1-wave kernel synchronises (igg/fused.hpp) — checked bitwise against the
-update_halo_ schedule on every rank over 24 graph-replayed steps, then A/B-timed
-(tiling x send mode x grid rounds); the faster schedule is kept.
+Multi-GPU: before anything is timed, every device transport / schedule
+(RCCL sequential, RCCL one-phase, one-sided put) is checked BITWISE against the
+host-staged gloo exchange (the reference's non-GPU-aware MPI path) on a
+rank-distinct payload with poisoned halo planes; failures are recorded in
+``config.validation`` and excluded. The survivors are A/B-timed on the model
+(hipGraph-replayed steps, MAX over ranks) and the fastest is kept; then the
+fused exchange (the stencil kernel stores its send planes into the
+neighbours' IPC-mapped arenas over xGMI; igg/fused.hpp) is checked bitwise
+against the chosen update_halo_ schedule over 24 steps and A/B-timed too.
+Every host wait on the GPU is bounded (IGG_COMM_TIMEOUT): a rank whose peer
+died aborts RCCL and fails instead of hanging.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--n 512]
                        [--dtype float64] [--overlap] [--variant V|auto]
-                       [--transport auto|rccl|put] [--no-graph]
+                       [--transport auto|rccl|put] [--no-graph] [--device gpu|cpu]
 """
 from __future__ import annotations
 
@@ -93,7 +101,84 @@ def parse():
                     help="fused halo exchange inside the stencil kernel (diffusion3d; auto: bitwise check + A/B)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on device 0, 'staged' instead of RCCL as the A/B reference")
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
+                    help="cpu: host fields and the gloo exchange (launch/plumbing check, no GPU needed)")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launch: seconds before the ranks are stopped and the run fails")
     return ap.parse_args()
+
+
+def self_launch(args) -> int:
+    """``--gpus N`` without a launcher: start N ranks of this script (one per
+    GPU, LOCAL_RANK = GPU index) from this parent, which never touches the GPU
+    (it does not even import torch). Fail-fast: the first rank that exits
+    non-zero stops the others. Prints rank 0's JSON line; non-zero exit if any
+    rank failed, the run timed out, or the line's n_gpus differs from N."""
+    import socket
+    import subprocess
+    import tempfile
+
+    n = args.gpus
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs, outs = [], []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), IGG_BENCH_SELF_LAUNCHED="1")
+        out = tempfile.TemporaryFile(mode="w+")
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env, stdout=out, stderr=None))
+    deadline = time.monotonic() + args.launch_timeout
+    rc, why = 0, ""
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                rc, why = 1, f"rank {bad[0][0]} exited with {bad[0][1]}"
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.monotonic() > deadline:
+                rc, why = 1, f"timed out after {args.launch_timeout:.0f} s"
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        rc, why = 130, "interrupted"
+    for p in procs:  # exact child processes of this parent, never by pattern
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=15)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    outs[0].seek(0)
+    lines = outs[0].read().splitlines()
+    for o in outs:
+        o.close()
+    rec = None
+    for ln in lines:
+        if ln.startswith("{") and '"metric"' in ln:
+            rec = ln
+        else:
+            print(ln, file=sys.stderr)
+    if rc != 0:
+        print(f"bench self-launch: {why}", file=sys.stderr)
+        return rc
+    if rec is None:
+        print("bench self-launch: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    got = json.loads(rec).get("n_gpus")
+    if got != n:
+        print(f"bench self-launch: result reports n_gpus={got}, expected {n}", file=sys.stderr)
+        return 1
+    print(rec, flush=True)
+    return 0
 
 
 def _max_over_ranks(comm, v: float) -> float:
@@ -106,67 +191,135 @@ def _max_over_ranks(comm, v: float) -> float:
     return float(t.item())
 
 
-def _timed(model, comm, k: int) -> float:
-    import torch
+def _sync(comm=None) -> None:
+    """Drain the GPU, bounded by IGG_COMM_TIMEOUT (aborts RCCL and raises
+    instead of hanging on a dead peer)."""
+    from igg.parallel.comm import bounded_device_sync
 
-    torch.cuda.synchronize()
+    bounded_device_sync(what="bench", comm=comm)
+
+
+def _timed(model, comm, k: int) -> float:
+    _sync(comm)
     comm.barrier()
     t0 = time.perf_counter()
-    for _ in range(k):
-        model.step()
-    torch.cuda.synchronize()
+    model.run(k)
+    _sync(comm)
     return _max_over_ranks(comm, time.perf_counter() - t0) / k
 
 
-def select_transport(model, field, comm, log, ref: str = "rccl") -> tuple[str, dict]:
-    """Bitwise cross-check put vs ``ref`` on the model's field, then A/B timing."""
+def _timed_candidate(model, comm, k: int, graph: bool) -> float:
+    """ms/step of the model's current schedule as the timed loop runs it:
+    hipGraph replays of captured steps (eager if capture is unsupported)."""
+    model.graph = None
+    model.step()
+    if graph:
+        try:
+            model.capture()
+        except Exception:
+            model.graph = None
+    return _timed(model, comm, k)
+
+
+def _probe_field(field):
+    """Rank-distinct payload (exact in fp64) with every boundary plane poisoned,
+    so a missing, misplaced or wrong-rank receive cannot go unnoticed."""
+    import torch
+
+    from igg.parallel.grid import global_grid
+
+    me = int(global_grid().me)
+    X = torch.arange(field.numel(), dtype=torch.float64, device=field.device).view(field.shape)
+    X += float(me + 1) * 2.0 ** 30
+    X = X.to(field.dtype)
+    for d in range(field.dim()):
+        X.select(d, 0).fill_(-7.0)
+        X.select(d, field.shape[d] - 1).fill_(-7.0)
+    return X
+
+
+# (name, transport, halo schedule) checked and A/B-timed at N > 1
+TRANSPORT_CANDIDATES = (("rccl-sequential", "rccl", "sequential"),
+                        ("rccl-onephase", "rccl", "onephase"),
+                        ("put", "put", "auto"))
+
+
+def validate_transports(field, comm, log, ref: str = "staged", names=None) -> dict:
+    """Bitwise check of every device transport / schedule against the
+    host-staged gloo exchange. Returns {name: "ok" | reason}; collective, and
+    every rank agrees (a failure on any rank fails the candidate)."""
     import torch
 
     from igg.parallel import halo as H
 
-    A, B = field.clone(), field.clone()
+    X0 = _probe_field(field)
     H.set_transport(ref)
-    H.update_halo_(A)
-    ok = False
-    try:
-        H.set_transport("put")  # collective: raises on every rank if a peer cannot be mapped
-        H.update_halo_(B)
-        torch.cuda.synchronize()
-        ok = bool(torch.equal(A, B))
-        H.check_transport()
-    except Exception as e:  # no IPC mapping, or a bounded spin timed out: put does not work here
-        log(f"put transport failed its check: {type(e).__name__}: {e}"[:300])
-        if getattr(comm, "mesh", None) is not None:
-            comm.mesh.clear_error()
-        ok = False
-        H.set_transport(ref)
-    bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
-    del A, B
-    times = {}
-    cands = [(ref, False)] + ([("put", False)] if bad == 0.0 else [])
+    H.set_halo_mode("sequential")
+    R = X0.clone()
+    H.update_halo_(R)
+    _sync(comm)
+    out = {}
+    for name, t, mode in TRANSPORT_CANDIDATES:
+        if names is not None and name not in names:
+            continue
+        why = ""
+        try:
+            H.set_transport(t)  # collective: creates the RCCL communicator / put mesh on first use
+            H.set_halo_mode(mode)
+            X = X0.clone()
+            H.update_halo_(X)
+            _sync(comm)
+            H.check_transport()
+            if not torch.equal(X, R):
+                bad = (X != R).nonzero()
+                why = f"mismatch at {bad.shape[0]} entries, first {bad[0].tolist()}"
+            del X
+        except Exception as e:  # e.g. no IPC mapping between these GPUs, a bounded spin timed out
+            why = f"{type(e).__name__}: {e}"[:300]
+            if getattr(comm, "mesh", None) is not None:
+                comm.mesh.clear_error()
+        fails = _max_over_ranks(comm, 1.0 if why else 0.0)
+        out[name] = "ok" if fails == 0.0 else (why or "failed on another rank")
+        log(f"validation {name} vs {ref}: {out[name]}")
+    H.set_transport("rccl" if out.get("rccl-sequential") == "ok" else ref)
+    H.set_halo_mode("auto")
+    del X0, R
+    return out
+
+
+def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, dict]:
+    """A/B timing of the validated transports / schedules on the model's step
+    (graph replays, MAX over ranks); keeps the fastest."""
+    from igg.parallel import halo as H
+
+    cands = [(name, t, mode, False) for name, t, mode in TRANSPORT_CANDIDATES if valid.get(name) == "ok"]
     # Overlap (boundary planes first, exchange on a second stream next to the
     # interior) only pays without z-neighbours: x/y boundary planes are cheap
     # rows, z-planes of a C-ordered field are maximally strided. RCCL's p2p
     # kernels stall next to a full-GPU stencil, so only put is tried overlapped.
-    if bad == 0.0 and getattr(model, "can_overlap", False) and not any(model.sides[2]):
-        cands.append(("put", True))
-    for t, ov in cands:
+    if valid.get("put") == "ok" and getattr(model, "can_overlap", False) and not any(model.sides[2]):
+        cands.append(("put+overlap", "put", "auto", True))
+    if not cands:
+        raise RuntimeError("no device transport passed the bitwise validation against the host-staged path")
+    times = {}
+    for name, t, mode, ov in cands:
         H.set_transport(t)
+        H.set_halo_mode(mode)
         if hasattr(model, "set_overlap"):
             model.set_overlap(ov)
-        model.step()
-        times[f"{t}{'+overlap' if ov else ''}"] = (_timed(model, comm, 10), t, ov)
+        times[name] = (_timed_candidate(model, comm, 20, graph), t, mode, ov)
     best = min(times, key=lambda k: times[k][0])
-    _, t, ov = times[best]
+    _, t, mode, ov = times[best]
     H.set_transport(t)
+    H.set_halo_mode(mode)
     if hasattr(model, "set_overlap"):
         model.set_overlap(ov)
-    log(f"schedule A/B (ms/step): {', '.join(f'{k}={v[0] * 1e3:.4f}' for k, v in times.items())}"
-        f"{'' if bad == 0.0 else ' (put mismatched rccl: excluded)'} -> {best}")
+    model.graph = None
+    log(f"schedule A/B (ms/step): {', '.join(f'{k}={v[0] * 1e3:.4f}' for k, v in times.items())} -> {best}")
     return best, {k: round(v[0] * 1e3, 5) for k, v in times.items()}
 
 
-def select_fused(model, comm, log, mode: str) -> dict | None:
+def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None:
     """Fused halo exchange (stencil stores the send planes into the neighbours'
     arenas; igg/fused.hpp) vs the schedule chosen so far: bitwise check of 24
     steps from the same state on every rank, then A/B timing (MAX over ranks).
@@ -191,7 +344,7 @@ def select_fused(model, comm, log, mode: str) -> dict | None:
         model.run(nchk - 1)
         model.graph = None
         model.sync_halo()
-        torch.cuda.synchronize()
+        _sync(comm)
         model.check()
         ok = bool(torch.equal(ref, model.T))
     except Exception as e:  # e.g. a sync kernel timed out: the fused path does not work here
@@ -211,17 +364,17 @@ def select_fused(model, comm, log, mode: str) -> dict | None:
     t_unf, times = float("inf"), {}
     for _ in range(2):
         model.set_fused(False)
-        model.step()
-        t_unf = min(t_unf, _timed(model, comm, 20))
+        t_unf = min(t_unf, _timed_candidate(model, comm, 20, graph))
         model.set_fused(True)
         for v, fm, gr in FUSED_CANDIDATES:
             model.fused_variant, model.fused_mode, model.fused_rounds = v, fm, gr
-            model.step()
-            times[(v, fm, gr)] = min(times.get((v, fm, gr), float("inf")), _timed(model, comm, 20))
+            t = _timed_candidate(model, comm, 20, graph)
+            times[(v, fm, gr)] = min(times.get((v, fm, gr), float("inf")), t)
     best, t_fus = min(times.items(), key=lambda kv: kv[1])
     model.fused_variant, model.fused_mode, model.fused_rounds = best
     keep = mode == "on" or t_fus < t_unf
     model.set_fused(keep)
+    model.graph = None
     name = lambda k: f"v{k[0]}/m{k[1]}/r{k[2]}"  # noqa: E731
     log(f"fused A/B (ms/step): update_halo={t_unf * 1e3:.4f}, "
         + ", ".join(f"fused {name(k)}={t * 1e3:.4f}" for k, t in times.items())
@@ -233,9 +386,13 @@ def select_fused(model, comm, log, mode: str) -> dict | None:
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(self_launch(args))
+    world = int(world_env or "1")
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report an "
+                         f"{world}-process number as an {args.gpus}-GPU one")
     import torch
 
     import igg
@@ -251,6 +408,7 @@ def main():
     n = args.n or cfg["n"]
     gather_every = cfg["gather_every"] if args.gather_every is None else args.gather_every
     is2d = cfg["model"] == "acoustic2d"
+    on_gpu = args.device == "gpu"
     pdims = "xyz" if args.periodic else (args.periodic_dims or "")
     if set(pdims) - set("xyz"):
         raise SystemExit(f"--periodic-dims: expected a subset of 'xyz', got {pdims!r}")
@@ -261,43 +419,64 @@ def main():
     os.environ.setdefault("IGG_PUT_TIMEOUT", "20")
     if args.share_gpu:
         os.environ.setdefault("IGG_TRANSPORT", "staged")
-    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, 1 if is2d else n, periodx=perx, periody=pery,
-                                                         periodz=0 if is2d else perz, quiet=True,
-                                                         select_device=not args.share_gpu)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(
+        n, n, 1 if is2d else n, periodx=perx, periody=pery, periodz=0 if is2d else perz, quiet=True,
+        select_device=on_gpu and not args.share_gpu, device_type="auto" if on_gpu else "none")
+    if nprocs != args.gpus:
+        raise SystemExit(f"bench: the grid has {nprocs} ranks, --gpus is {args.gpus}")
     log = (lambda m: print(m, file=sys.stderr, flush=True)) if me == 0 else (lambda m: None)
+    if on_gpu and not torch.cuda.is_available():
+        raise SystemExit("bench: no GPU visible (use --device cpu for a plumbing run)")
     if args.loopback:
         lb = (bool(perx), bool(pery), bool(perz)) if pdims else (True, True, True)
         H.enable_loopback((lb[0], lb[1], lb[2] and not is2d))
-    model = Acoustic2D(dtype=dtype) if is2d else Diffusion3D(dtype=dtype, overlap=args.overlap)
+    dev = None if on_gpu else "cpu"
+    model = Acoustic2D(dtype=dtype) if is2d else Diffusion3D(dtype=dtype, overlap=args.overlap, device=dev)
     field = (lambda: model.P) if is2d else (lambda: model.T)
+    sync = (lambda: _sync(comm)) if on_gpu else (lambda: None)
     A_global = None
     if gather_every > 0 and me == 0:
         # gather_ concatenates the local blocks (halos included) in Cartesian order
         A_global = torch.empty([int(d) * int(s) for d, s in zip(dims, field().shape)],
                                dtype=dtype, device=field().device)
-    ab = None
-    if nprocs > 1 and args.transport == "auto" and not args.overlap:
-        _, ab = select_transport(model, field(), comm, log, ref="staged" if args.share_gpu else "rccl")
+    graph_ok = args.graph and on_gpu
+    valid, ab = None, None
+    if on_gpu and nprocs > 1:
+        ref = "staged"
+        names = None if args.transport == "auto" else [c[0] for c in TRANSPORT_CANDIDATES if c[1] == args.transport]
+        if args.share_gpu:  # ranks share one device: RCCL refuses duplicate GPUs
+            names = ["put"]
+        valid = validate_transports(field(), comm, log, ref=ref, names=names)
+        if args.share_gpu and valid.get("put") != "ok":
+            H.set_transport("staged")
+        elif not args.overlap:
+            _, ab = select_transport(model, comm, log, valid, graph_ok)
+        elif any(v == "ok" for v in valid.values()):
+            first = next(c for c in TRANSPORT_CANDIDATES if valid.get(c[0]) == "ok")
+            H.set_transport(first[1])
+            H.set_halo_mode(first[2])
+        else:
+            raise RuntimeError("no device transport passed the bitwise validation")
     fused_ab = None
-    if not is2d and not args.overlap and (nprocs > 1 or args.loopback or pdims):
-        fused_ab = select_fused(model, comm, log, args.fused)
+    if on_gpu and not is2d and not args.overlap and (nprocs > 1 or args.loopback or pdims):
+        fused_ab = select_fused(model, comm, log, args.fused, graph_ok)
     for _ in range(args.warmup):
         model.step()
     graph_error = None
-    if args.graph:
+    if graph_ok:
         try:
             model.capture()
         except Exception as e:  # capture unsupported here: time eager steps
             graph_error = f"{type(e).__name__}: {e}"[:200]
             model.graph = None
             log(f"hipGraph capture failed, running eager: {graph_error}")
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     if gather_every > 0:
         done, pending = 0, None
-        snap = torch.empty_like(field()) if args.gather_mode == "async" else None
+        snap = torch.empty_like(field()) if args.gather_mode == "async" and on_gpu else None
         while done < args.steps:
             k = min(gather_every, args.steps - done)
             model.run(k)
@@ -316,7 +495,7 @@ def main():
             pending.wait()
     else:
         model.run(args.steps)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
     t1 = time.perf_counter()
     elapsed = _max_over_ranks(comm, t1 - t0)
@@ -330,7 +509,7 @@ def main():
         model.sync_halo()
     finite = bool(torch.isfinite(field()).all().item())
     phase_ms = None
-    if not is2d and nprocs > 1 or args.loopback:
+    if on_gpu and (not is2d and nprocs > 1 or args.loopback):
         # stencil vs halo split of a few eager steps (events on the stream)
         from igg.utils.trace import PhaseTimer
 
@@ -341,13 +520,13 @@ def main():
         model.timer = None
     gather_ms = None
     if gather_every > 0:
-        torch.cuda.synchronize()
+        sync()
         comm.barrier()
         tg = time.perf_counter()
         if getattr(model, "fused", False):
             model.sync_halo()
         igg.gather_(field(), A_global)
-        torch.cuda.synchronize()
+        sync()
         gather_ms = round(_max_over_ranks(comm, time.perf_counter() - tg) * 1e3, 3)
     if me == 0:
         out = {
@@ -369,6 +548,9 @@ def main():
                 "global_batch": nprocs,
                 "seq_len": n,
                 "parallelism": f"spatial {dims[0]}x{dims[1]}x{dims[2]}",
+                "value_semantics": "whole-job aggregate T_eff = sum over the n_gpus GPUs (bench contract); "
+                                   "per-GPU T_eff in t_eff_per_gpu_GBs",
+                "device": args.device,
                 "local_grid": [n, n] if is2d else [n, n, n],
                 "global_grid": [int(v) for v in igg.get_global_grid().nxyz_g],
                 "overlap_comm": bool(getattr(model, "overlap", False)),
@@ -376,9 +558,15 @@ def main():
                 "gather_ms": gather_ms,
                 "gather_mode": args.gather_mode if gather_every > 0 else None,
                 "phase_ms": phase_ms,
+                "t_it_ms": round(t_it * 1e3, 5),
                 "t_eff_per_gpu_GBs": round(per_gpu, 3),
+                "t_eff_aggregate_GBs": round(total, 3),
                 "a_eff_bytes_per_gpu": model.a_eff_bytes,
                 "transport": H.transport_name(),
+                "halo_schedule": (H.plan_mode(field()) if H.transport_name() != "put" else "put")
+                if nprocs > 1 or args.loopback else None,
+                "halo_mode_measured": H.tuned_modes() or None,
+                "validation": valid,
                 "transport_ab_ms": ab,
                 "fused_halo": bool(getattr(model, "fused", False)),
                 "fused_kernel": ({"variant": model.fused_variant, "mode": model.fused_mode,
@@ -389,7 +577,8 @@ def main():
                 "stencil_variant_ms": getattr(model, "variant_times", None),
                 "finite": finite,
                 "loopback_emulation": bool(args.loopback),
-                "hip_graph": model.graph is not None,
+                "self_launched": os.environ.get("IGG_BENCH_SELF_LAUNCHED") == "1",
+                "hip_graph": getattr(model, "graph", None) is not None,
                 "hip_graph_error": graph_error,
             },
         }

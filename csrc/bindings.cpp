@@ -180,6 +180,8 @@ PYBIND11_MODULE(_igg_native, m) {
     stream_wait_u64_geq(as_stream(s), reinterpret_cast<void*>(p), v);
   });
   m.def("can_stream_wait_value", &can_stream_wait_value);
+  m.def("gpu_spin", [](double seconds, uintptr_t s) { launch_spin(seconds, as_stream(s)); },
+        py::arg("seconds"), py::arg("stream"));
   m.def("read_u64", [](uintptr_t p) {
     uint64_t v = 0;
     IGG_HIP_CHECK(hipMemcpy(&v, reinterpret_cast<void*>(p), 8, hipMemcpyDeviceToHost));
@@ -359,7 +361,8 @@ PYBIND11_MODULE(_igg_native, m) {
       })
       .def_property_readonly("last_message_count", &HaloEngine::last_message_count)
       .def("exchange_set",
-           [](HaloEngine& e, const FieldSet& fs, uintptr_t s) { e.exchange(fs.f, as_stream(s)); })
+           [](HaloEngine& e, const FieldSet& fs, uintptr_t s, int mode) { e.exchange(fs.f, as_stream(s), mode); },
+           py::arg("fields"), py::arg("stream"), py::arg("mode") = -1)
       .def("exchange_dim",
            [](HaloEngine& e, const std::vector<FieldTuple>& fs, int dim, uintptr_t s) {
              e.exchange_dim(to_fields(fs), dim, as_stream(s));

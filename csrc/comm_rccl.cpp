@@ -61,20 +61,31 @@ RcclComm::~RcclComm() {
 void RcclComm::exchange(const std::vector<P2POp>& recvs, const std::vector<P2POp>& sends,
                         bool device, hipStream_t stream) {
   if (!device) fail("RCCL transport can only move device (GPU) memory.");
+  if (aborted_) fail("RCCL communicator was aborted after a communication failure (IGG_COMM_TIMEOUT); "
+                     "re-initialise the grid.");
   if (recvs.empty() && sends.empty()) return;
   IGG_NCCL_CHECK(ncclGroupStart());
-  for (const P2POp& r : recvs)
-    IGG_NCCL_CHECK(ncclRecv(r.ptr, r.bytes, ncclUint8, r.peer, comm_, stream));
-  for (const P2POp& s : sends)
-    IGG_NCCL_CHECK(ncclSend(s.ptr, s.bytes, ncclUint8, s.peer, comm_, stream));
+  try {
+    for (const P2POp& r : recvs)
+      IGG_NCCL_CHECK(ncclRecv(r.ptr, r.bytes, ncclUint8, r.peer, comm_, stream));
+    for (const P2POp& s : sends)
+      IGG_NCCL_CHECK(ncclSend(s.ptr, s.bytes, ncclUint8, s.peer, comm_, stream));
+  } catch (...) {
+    // Never leave the thread's RCCL group open: a later group would nest into
+    // it and hang. The group's own error (if any) is secondary to the first.
+    (void)ncclGroupEnd();
+    throw;
+  }
   IGG_NCCL_CHECK(ncclGroupEnd());
 }
 
 void RcclComm::barrier(hipStream_t stream) {
+  if (aborted_) fail("RCCL communicator was aborted");
   IGG_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, stream));
 }
 
 void RcclComm::check_async_error() {
+  if (aborted_) fail("RCCL communicator was aborted after a communication failure");
   ncclResult_t st = ncclSuccess;
   IGG_NCCL_CHECK(ncclCommGetAsyncError(comm_, &st));
   if (st != ncclSuccess && st != ncclInProgress)

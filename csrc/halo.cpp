@@ -198,7 +198,7 @@ HaloEngine::~HaloEngine() {
   if (done_) (void)hipEventDestroy(done_);
 }
 
-void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) {
+void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream, int mode_override) {
   if (fields.empty()) return;
   TraceRange tr("igg.update_halo");
   const bool device = fields[0].device;
@@ -229,7 +229,8 @@ void HaloEngine::exchange(const std::vector<Field>& fields, hipStream_t stream) 
     // Kernel arguments are epoch-independent (the epoch lives on the device),
     // so a captured exchange replays correctly.
     exchange_put(fields, stream, put->mesh());
-  } else if (resolved_mode(fields) == HaloMode::OnePhase) {
+  } else if ((mode_override >= 0 ? static_cast<HaloMode>(mode_override) : resolved_mode(fields)) ==
+             HaloMode::OnePhase) {
     exchange_onephase(fields, device, stream);
   } else {
     last_msgs_ = 0;
@@ -382,15 +383,13 @@ bool HaloEngine::active(const Field& f, int d) const {
 }
 
 HaloMode HaloEngine::resolved_mode(const std::vector<Field>& fields) const {
-  if (mode_ != HaloMode::Auto) return mode_;
-  if (!grid_.has_peers) return HaloMode::Sequential;
-  for (int d = 0; d < NDIMS; ++d)
-    for (int s = 0; s < NNEIGHBORS; ++s) {
-      const int64_t nb = grid_.neighbors[s][d];
-      if (nb != PROC_NULL && nb != grid_.me) return HaloMode::OnePhase;
-    }
+  // Auto without a measurement: the sequential x -> y -> z schedule (3 RCCL
+  // groups of <= 2 peers). One-phase (one group, up to 26 peers incl. edges and
+  // corners) measured 2x slower on the 1-GPU loopback of a 512^3 field
+  // (profiles/r1_graph/lb_one.log vs lb_seq.log); parallel/halo.py times both
+  // per field set on first use and passes the winner as mode_override.
   (void)fields;
-  return HaloMode::Sequential;
+  return mode_ == HaloMode::Auto ? HaloMode::Sequential : mode_;
 }
 
 namespace {

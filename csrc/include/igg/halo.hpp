@@ -147,14 +147,17 @@ class HaloEngine {
   BufferPool& pool() { return pool_; }
 
   // Full update_halo! of `fields` (validated by the caller), stream-ordered.
-  void exchange(const std::vector<Field>& fields, hipStream_t stream);
+  // `mode_override` >= 0 forces a schedule for this call (a measured per-field-
+  // set choice of parallel/halo.py); -1 uses set_mode / Auto.
+  void exchange(const std::vector<Field>& fields, hipStream_t stream, int mode_override = -1);
   // Only the dimension `dim` (0-based); used by tests and pipelined apps.
   void exchange_dim(const std::vector<Field>& fields, int dim, hipStream_t stream);
   void set_mode(HaloMode m) { mode_ = m; }
   HaloMode mode() const { return mode_; }
   void set_pack_mode(int dim, PackMode m) { pack_mode_.at(static_cast<size_t>(dim)) = m; }
   PackMode pack_mode(int dim) const { return pack_mode_.at(static_cast<size_t>(dim)); }
-  // Mode the next exchange of `fields` would use (Auto resolved).
+  // Mode the next exchange of `fields` would use (Auto resolved: Sequential,
+  // the schedule measured faster by default; halo.py measures per field set).
   HaloMode resolved_mode(const std::vector<Field>& fields) const;
   int last_message_count() const { return last_msgs_; }
 

@@ -51,5 +51,7 @@ struct PutSync {
 void launch_put_begin(const PutSync& s, hipStream_t stream);
 void launch_put_sync(const PutSync& s, hipStream_t stream);
 int64_t put_timeout_ticks(double seconds);
+// One wave spinning `seconds` of wall-clock time on `stream` (failure-path tests).
+void launch_spin(double seconds, hipStream_t stream);
 
 }  // namespace igg

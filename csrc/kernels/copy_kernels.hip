@@ -68,10 +68,24 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
       if (i < n) dst[i * cp.dst_si] = v[k];
     }
   }
-  // Put transport: the destination arena is uncached (stores bypass L2), so
-  // waiting for this thread's stores to be acknowledged is all the release
-  // needed before the sync kernel publishes the arrival flag.
-  if (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  // Put transport, cross-device ordering argument (writer side):
+  //  1. the destination arena is IPC-mapped peer memory allocated uncached
+  //     (MemKind::Uncached: MTYPE UC), so these stores bypass this GPU's L2
+  //     and travel over xGMI to the owner's HBM; there is no dirty line to
+  //     write back at any scope;
+  //  2. s_waitcnt vmcnt(0) below holds the wave until every one of its stores
+  //     has been acknowledged by the memory system that owns the address
+  //     (for a remote address: after the write reached the peer's fabric /
+  //     memory controller). A workgroup-scope release fence would NOT wait
+  //     for this on gfx9 outside tgsplit mode, hence the explicit wait;
+  //  3. the sync kernel runs after this kernel on the same in-order stream
+  //     (AQL barrier bit: it starts only once every wave here retired), issues
+  //     __threadfence_system() and only then stores the ARRIVED flag into the
+  //     receiver's flag words with a system-scope release;
+  //  4. the receiver's sync kernel observes the flag with a system-scope
+  //     acquire load; its unpack kernel reads the (uncached) arena after that
+  //     kernel on the same stream, so it cannot see pre-put data.
+  if (FENCE) __builtin_amdgcn_s_waitcnt(0);
 }
 
 template <typename T, bool FENCE>

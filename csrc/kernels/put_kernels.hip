@@ -54,11 +54,28 @@ __global__ void __launch_bounds__(64) put_sync_kernel(const PutSync s) {
   if (lane < s.n_out) store_sys(s.out_flags[lane] + PutFlags::ARRIVED + s.my_rank, e);
   if (lane < s.n_in && !wait_geq(s.my_flags + PutFlags::ARRIVED + s.in_rank[lane], e, s, 0x200 + lane)) ok = 0;
   __syncthreads();
+  // A timed-out wait (ok == 0) already left its code in the sticky ERROR word
+  // (wait_geq); the epoch still advances so the stream drains instead of
+  // hanging the GPU. The host reports it at the next check_transport() /
+  // update_halo_ poll (IGG_POLL_EVERY) / finalize, never silently.
   (void)ok;
   if (lane == 0) store_sys(s.my_flags + PutFlags::EPOCH, e);  // exchange e complete (unpack reads parity e)
 }
 
+// Failure-path test aid: one wave that spins for `ticks` wall-clock ticks (a
+// bounded stand-in for a kernel blocked on a peer that never answers).
+__global__ void __launch_bounds__(64) spin_kernel(int64_t ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(10);
+}
+
 }  // namespace
+
+void launch_spin(double seconds, hipStream_t stream) {
+  if (seconds < 0 || seconds > 60) fail("launch_spin: 0..60 s");
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, stream, put_timeout_ticks(seconds));
+  IGG_HIP_CHECK(hipGetLastError());
+}
 
 void launch_put_begin(const PutSync& s, hipStream_t stream) {
   if (s.n_out > 64 || s.n_nb > 64) fail("launch_put_begin: too many peers");

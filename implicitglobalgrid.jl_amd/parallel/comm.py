@@ -63,7 +63,7 @@ def runtime_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
-def init_runtime(timeout_s: float = 600.0) -> None:
+def init_runtime(timeout_s: float | None = None) -> None:
     """Initialise torch.distributed (the MPI.Init equivalent).
 
     With launcher environment variables (``WORLD_SIZE`` etc.) this joins the
@@ -72,6 +72,9 @@ def init_runtime(timeout_s: float = 600.0) -> None:
     """
     if runtime_initialized():
         raise IGGError("The distributed runtime is already initialized.")
+    # Every host collective is bounded (IGG_COMM_TIMEOUT, with a floor so a
+    # long first-use autotune on one rank never trips it).
+    timeout_s = max(60.0, config.comm_timeout()) if timeout_s is None else timeout_s
     timeout = datetime.timedelta(seconds=timeout_s)
     if "WORLD_SIZE" in os.environ and "RANK" in os.environ:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -105,6 +108,7 @@ class Communicator:
     local_rank: int = 0
     local_size: int = 1
     _transports: dict = field(default_factory=dict)
+    aborted: str = ""
 
     def __eq__(self, other):  # identity semantics like MPI.Comm handles
         return self is other
@@ -117,9 +121,67 @@ class Communicator:
         return dist.get_global_rank(self.gloo, r)
 
     # -- collectives -------------------------------------------------------
-    def barrier(self) -> None:
+    def barrier(self, timeout: float | None = None) -> None:
+        """Host barrier of all ranks, bounded by ``timeout`` seconds (default
+        IGG_COMM_TIMEOUT). On expiry the device communicators are aborted (a
+        peer blocked in an RCCL kernel is released) and IGGError is raised,
+        naming the ranks that did not arrive."""
+        if self.size <= 1:
+            return
+        t = config.comm_timeout() if timeout is None else float(timeout)
+        try:
+            dist.monitored_barrier(group=self.gloo, timeout=datetime.timedelta(seconds=t), wait_all_ranks=True)
+        except RuntimeError as e:
+            self.abort(f"barrier timed out after {t:.0f} s")
+            raise IGGError(f"barrier: not every rank arrived within {t:.0f} s (IGG_COMM_TIMEOUT); "
+                           f"device communicators aborted: {str(e).splitlines()[0][:300]}") from None
+
+    def abort(self, reason: str = "") -> None:
+        """Abort the device communicators (ncclCommAbort: RCCL kernels waiting
+        on a peer exit) after an unrecoverable communication failure; later
+        device exchanges raise instead of hanging."""
+        self.aborted = reason or "aborted"
+        if self.rccl is not None:
+            try:
+                self.rccl.abort()
+            except Exception:
+                pass
+
+    # -- tensor collectives (comm_cart interop) --------------------------------
+    # The reference hands applications its MPI Cartesian communicator for their
+    # own collectives (README.md:166-178: e.g. a global residual). Here: CPU
+    # tensors over gloo, GPU tensors over RCCL (torch's nccl backend) ordered on
+    # the caller's current stream.
+    _OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "prod": "PRODUCT"}
+
+    def _tensor_group(self, t: torch.Tensor):
+        if not t.is_cuda:
+            return self.gloo
+        self._ensure_torch_nccl()
+        return self.torch_nccl
+
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """In-place all-reduce of ``t`` over the grid's ranks (``op``: sum,
+        max, min, prod); returns ``t``. MPI.Allreduce! on comm_cart."""
+        if op not in self._OPS:
+            raise IGGError(f"allreduce_: op must be one of {sorted(self._OPS)} (got {op!r})")
         if self.size > 1:
-            dist.barrier(group=self.gloo)
+            dist.all_reduce(t, op=getattr(dist.ReduceOp, self._OPS[op]), group=self._tensor_group(t))
+        return t
+
+    def bcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        """In-place broadcast of ``t`` from grid rank ``root``; returns ``t``
+        (MPI.Bcast! on comm_cart)."""
+        if not 0 <= root < self.size:
+            raise IGGError(f"bcast_: root {root} out of range 0..{self.size - 1}")
+        if self.size > 1:
+            dist.broadcast(t, src=self.global_rank(root), group=self._tensor_group(t))
+        return t
+
+    def allreduce(self, value: float, op: str = "sum") -> float:
+        """All-reduce of a Python scalar (host), e.g. a global residual norm."""
+        t = torch.tensor([float(value)], dtype=torch.float64)
+        return float(self.allreduce_(t, op).item())
 
     def broadcast_object(self, obj, root: int = 0):
         if self.size == 1:
@@ -264,6 +326,40 @@ class Communicator:
             except Exception:
                 pass
         self.gloo = None
+
+
+def bounded_device_sync(timeout: float | None = None, what: str = "device synchronize", comm=None) -> None:
+    """``hipDeviceSynchronize`` that gives up after ``timeout`` seconds
+    (default IGG_COMM_TIMEOUT): the wait runs in a helper thread; on expiry the
+    grid's device communicators are aborted (so RCCL kernels blocked on a
+    dead or diverged peer exit) and IGGError is raised. SURVEY §5.3: a rank
+    must never hang silently on a peer that will not answer."""
+    import threading
+
+    t = config.comm_timeout() if timeout is None else float(timeout)
+    done = threading.Event()
+    err: list = []
+
+    def run():
+        try:
+            native.device_synchronize()
+        except Exception as e:  # surfaced on the caller's thread
+            err.append(e)
+        finally:
+            done.set()
+
+    th = threading.Thread(target=run, name="igg-bounded-sync", daemon=True)
+    th.start()
+    if not done.wait(t):
+        if comm is not None:
+            comm.abort(f"{what} timed out after {t:.0f} s")
+        from . import halo as _halo
+
+        _halo.abort_loopback()
+        raise IGGError(f"{what}: the GPU did not drain within {t:.0f} s (IGG_COMM_TIMEOUT): a peer rank "
+                       "is probably dead or skipped a collective exchange; device communicators aborted.")
+    if err:
+        raise err[0]
 
 
 def make_communicator(group=None) -> Communicator:

@@ -263,16 +263,27 @@ def finalize_global_grid(*, finalize_MPI: bool = True) -> None:
     from . import gather as _gather
     from . import halo as _halo
 
-    _halo.check_transport()
-    _gather.free_gather_buffer()
-    _halo.free_update_halo_buffers()
+    if finalize_MPI and not _comm.runtime_initialized():
+        raise IGGError("MPI cannot be finalized as it has not been initialized. ")
+    # A transport error (a put sync kernel that timed out, an asynchronous RCCL
+    # failure) is reported AFTER everything is released: finalize must always
+    # leave the grid reset, or neither a re-init nor a second finalize could
+    # succeed and buffers / communicators would leak.
+    transport_error = None
+    try:
+        _halo.check_transport()
+    except IGGError as e:
+        transport_error = e
     gg = _global_grid
-    _halo._drop_engine()
-    if finalize_MPI:
-        if not _comm.runtime_initialized():
-            raise IGGError("MPI cannot be finalized as it has not been initialized. ")
-    if gg.comm is not None:
-        gg.comm.destroy()
-    if finalize_MPI:
-        _comm.finalize_runtime()
-    set_global_grid(GLOBAL_GRID_NULL)
+    try:
+        _gather.free_gather_buffer()
+        _halo.free_update_halo_buffers()
+        _halo._drop_engine()
+        if gg.comm is not None:
+            gg.comm.destroy()
+        if finalize_MPI:
+            _comm.finalize_runtime()
+    finally:
+        set_global_grid(GLOBAL_GRID_NULL)
+    if transport_error is not None:
+        raise transport_error

@@ -118,6 +118,8 @@ def set_halo_mode(mode: str) -> None:
     algorithm), 'onephase' (faces+edges+corners in one phase) or 'auto'."""
     _grid.check_initialized()
     _engine.set_mode(HALO_MODES[mode])
+    for p in _plans.values():
+        p[3] = None  # an explicit mode wins; 'auto' measures again
 
 
 def halo_mode() -> str:
@@ -152,10 +154,19 @@ def _init_engine(gg) -> None:
     for d, m in enumerate(config.pack_modes()):
         _engine.set_pack_mode(d, config.PACK_MODES.index(m))
     _debug_sync = config.debug_sync()
+    _set_poll_every(config.poll_every())
     if gg.nprocs > 1:
         _engine.set_transport(gg.comm.host_transport(), False)
         if gg.amdgpu_enabled:
             _engine.set_transport(gg.comm.device_transport(), True)
+
+
+_poll_every = 1000
+
+
+def _set_poll_every(n: int) -> None:
+    global _poll_every, _poll_count
+    _poll_every, _poll_count = int(n), 0
 
 
 def _drop_engine() -> None:
@@ -178,6 +189,8 @@ def set_transport(name: str) -> None:
     if not gg.amdgpu_enabled:
         raise IGGError("set_transport: the grid was not initialised for GPU fields")
     _engine.set_transport(gg.comm.device_transport(name), True)
+    for p in _plans.values():
+        p[3] = None  # schedule costs differ per transport: 'auto' measures again
 
 
 def transport_name() -> str:
@@ -204,6 +217,15 @@ def check_transport() -> None:
     for c in rcc:
         if c is not None:
             c.check_async_error()  # ncclCommGetAsyncError: raises on an asynchronous RCCL failure
+
+
+def abort_loopback() -> None:
+    """Abort the single-GPU loopback RCCL communicator (bounded-wait expiry)."""
+    if _loopback_comm is not None and isinstance(_loopback_comm, native.RcclComm):
+        try:
+            _loopback_comm.abort()
+        except Exception:
+            pass
 
 
 def engine():
@@ -319,9 +341,73 @@ def _plan(fields):
             )
         if len(_plans) >= _MAX_PLANS:
             _plans.clear()
-        p = (native.FieldSet([field_tuple(A) for A in fields]), device, fields[0].dtype)
+        p = [native.FieldSet([field_tuple(A) for A in fields]), device, fields[0].dtype, None]
         _plans[key] = p
     return p
+
+
+# --- measured schedule choice ('auto' mode) -----------------------------------
+# Timed exchanges per schedule (after one untimed warm-up exchange each, which
+# also opens RCCL's lazily connected peer channels).
+_TUNE_REPS = 5
+_tuned_log: list = []  # (field shapes, {mode: ms}, winner) of every measurement
+
+
+def _remote_peers() -> bool:
+    """A device exchange of this grid reaches another rank (or the loopback
+    emulation): only then do the schedules differ in cost."""
+    gg = _grid.global_grid()
+    if _loopback_comm is not None:
+        return True
+    nb = gg.neighbors
+    return bool(((nb != PROC_NULL) & (nb != gg.me)).any())
+
+
+def _tune_mode(fs, stream: int) -> int:
+    """Time the sequential and one-phase schedules on this field set (MAX over
+    ranks, so every rank picks the same winner) and return the faster mode.
+    Collective like update_halo_ itself. Safe to run on live data: a halo
+    exchange is idempotent (send planes are interior, receive planes halo)."""
+    import time
+
+    gg = _grid.global_grid()
+    times = {}
+    for name in ("sequential", "onephase"):
+        m = HALO_MODES[name]
+        _engine.exchange_set(fs, stream, m)
+        native.stream_synchronize(stream)
+        if gg.comm is not None:
+            gg.comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(_TUNE_REPS):
+            _engine.exchange_set(fs, stream, m)
+        native.stream_synchronize(stream)
+        dt = (time.perf_counter() - t0) / _TUNE_REPS
+        if gg.comm is not None and gg.comm.size > 1:
+            import torch.distributed as dist
+
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=gg.comm.gloo)
+            dt = float(t.item())
+        times[name] = dt
+    win = min(times, key=times.get)
+    _tuned_log.append(({k: round(v * 1e3, 4) for k, v in times.items()}, win))
+    return HALO_MODES[win]
+
+
+def tuned_modes() -> list:
+    """Measurements of the 'auto' schedule choice so far: ``[({mode: ms}, winner), ...]``."""
+    return list(_tuned_log)
+
+
+def plan_mode(*fields) -> str:
+    """Schedule the next ``update_halo_(*fields)`` uses: the measured winner for
+    this field set if 'auto' measured one, else the engine's mode (auto
+    without a measurement resolves to sequential)."""
+    p = _plan(fields)
+    if p[3] is not None:
+        return {v: k for k, v in HALO_MODES.items()}[p[3]]
+    return {v: k for k, v in HALO_MODES.items()}[_engine.resolved_mode(p[0])]
 
 
 def update_halo_(*fields) -> None:
@@ -330,16 +416,43 @@ def update_halo_(*fields) -> None:
     Group fields in one call for better performance: every dimension then needs
     one pack launch, one communication phase and one unpack launch for all of
     them. GPU work is stream-ordered on ``torch.cuda.current_stream()``.
+
+    Schedule ('auto', the default): the first eager exchange of a GPU field set
+    that reaches other ranks times the sequential and the one-phase schedule
+    (collectively; a few extra exchanges) and keeps the faster for that field
+    set; later calls and hipGraph captures reuse the choice.
     """
     _grid.check_initialized()
     if not fields:
         return
-    fs, device, dtype = _plan(fields)
+    p = _plan(fields)
+    fs, device, dtype, mode = p
     stream = torch.cuda.current_stream().cuda_stream if device else 0
-    _engine.exchange_set(fs, stream)
+    if mode is None and device and _engine.mode == HALO_MODES["auto"]:
+        if _remote_peers() and _engine.transport_name(True) != "put" \
+                and not torch.cuda.is_current_stream_capturing():
+            mode = p[3] = _tune_mode(fs, stream)
+    _engine.exchange_set(fs, stream, -1 if mode is None or _engine.mode != HALO_MODES["auto"] else mode)
     _buf_dtype[device] = dtype
     if _debug_sync and device and not torch.cuda.is_current_stream_capturing():
         native.stream_synchronize(stream)
+    _poll_transport()
+
+
+_poll_count = 0
+
+
+def _poll_transport() -> None:
+    """Every IGG_POLL_EVERY exchanges (default 1000; 0 = never) read the put
+    transport's sticky error word on a side stream (no sync of the caller's
+    stream), so a timed-out synchronisation surfaces within a bounded number
+    of steps instead of only at check_transport()/finalize."""
+    global _poll_count
+    if _poll_every <= 0:
+        return
+    _poll_count += 1
+    if _poll_count % _poll_every == 0 and not torch.cuda.is_current_stream_capturing():
+        check_transport()
 
 
 update_halo = update_halo_

@@ -66,8 +66,19 @@ def save_checkpoint(prefix: str, step: int = 0, **fields: torch.Tensor) -> str:
     local = {"coords": json.dumps([int(c) for c in gg.coords]), "step": str(int(step))}
     path = _rank_file(prefix, me)
     tmp = path + ".tmp"
-    save_file(tensors, tmp, metadata=local)
-    os.replace(tmp, path)  # a crash mid-write never leaves a truncated checkpoint under the final name
+    err = ""
+    try:
+        save_file(tensors, tmp, metadata=local)
+        os.replace(tmp, path)  # a crash mid-write never leaves a truncated checkpoint under the final name
+    except Exception as e:  # reported collectively below, so no rank waits forever
+        err = f"{type(e).__name__}: {e}"
+    # The manifest names the step only once EVERY rank has its block on disk:
+    # a crash before this point leaves the previous manifest (and a step check
+    # in load_checkpoint catches a block that was not rewritten).
+    errs = gg.comm.all_gather_object(err) if gg.comm is not None else [err]
+    bad = [(r, e) for r, e in enumerate(errs) if e]
+    if bad:
+        raise IGGError(f"save_checkpoint: rank {bad[0][0]} failed to write its block: {bad[0][1]}")
     if me == 0:
         with open(prefix + ".json.tmp", "w") as f:
             json.dump(meta, f, indent=1, sort_keys=True)
@@ -109,6 +120,9 @@ def load_checkpoint(prefix: str, device=None) -> tuple[dict, dict]:
         if json.loads(local.get("coords", "null")) != [int(c) for c in gg.coords]:
             raise IGGError(f"load_checkpoint: {path} was written by the rank at coords {local.get('coords')}, "
                            f"this rank is at {[int(c) for c in gg.coords]}")
+        if str(local.get("step")) != str(meta["step"]):
+            raise IGGError(f"load_checkpoint: {path} holds step {local.get('step')}, the manifest names "
+                           f"step {meta['step']} (blocks from different saves)")
         names = set(f.keys())
         if names != set(meta["fields"]):
             raise IGGError(f"load_checkpoint: {path} holds fields {sorted(names)}, manifest {sorted(meta['fields'])}")

@@ -96,3 +96,18 @@ def pack_modes(env: Mapping[str, str] | None = None) -> list[str]:
 def debug_sync(env: Mapping[str, str] | None = None) -> bool:
     env = os.environ if env is None else env
     return env.get("IGG_DEBUG_SYNC", "0") not in ("", "0")
+
+
+def poll_every(env: Mapping[str, str] | None = None) -> int:
+    """``IGG_POLL_EVERY``: check the transports' asynchronous error state every
+    N update_halo_ calls (default 1000, 0 = only at check_transport/finalize)."""
+    env = os.environ if env is None else env
+    return int(env.get("IGG_POLL_EVERY", "1000"))
+
+
+def comm_timeout(env: Mapping[str, str] | None = None) -> float:
+    """``IGG_COMM_TIMEOUT``: seconds a host-side wait (barrier, tic/toc, eager
+    RCCL exchange) may block before the communicators are aborted and every
+    rank raises (default 300)."""
+    env = os.environ if env is None else env
+    return float(env.get("IGG_COMM_TIMEOUT", "300"))

@@ -11,6 +11,7 @@ import time
 
 import torch
 
+from ..parallel import comm as _comm
 from ..parallel import grid as _grid
 
 
@@ -89,7 +90,8 @@ _t0 = None
 def _sync_all() -> None:
     gg = _grid.global_grid()
     if gg.amdgpu_enabled and torch.cuda.is_available():
-        torch.cuda.synchronize()
+        # bounded (IGG_COMM_TIMEOUT): aborts RCCL and raises instead of hanging
+        _comm.bounded_device_sync(what="tic/toc", comm=gg.comm)
     gg.comm.barrier()
 
 

@@ -19,6 +19,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: test needs an MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "multigpu: needs several MI355X, one rank per device (tests/test_multigpu.py)")
 
 
 def _have_gpu() -> bool:

@@ -14,6 +14,11 @@ DTYPES = {"f64": torch.float64, "f32": torch.float32, "f16": torch.float16, "c12
 
 
 def _device(kind):
+    """cpu | gpu (every rank on device 0) | mgpu (one rank per device: LOCAL_RANK)."""
+    if kind == "mgpu":
+        r = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(r)
+        return torch.device("cuda", r)
     if kind == "gpu":
         torch.cuda.set_device(0)
         return torch.device("cuda", 0)
@@ -26,7 +31,7 @@ def scenario_halo(dev, nx, ny, nz, px, py, pz, dt, dimx=0, dimy=0, dimz=0):
     dtype = DTYPES[dt]
     igg.init_global_grid(nx, ny, nz, periodx=px, periody=py, periodz=pz, dimx=int(dimx), dimy=int(dimy),
                          dimz=int(dimz), quiet=True, select_device=False,
-                         device_type="AMDGPU" if dev == "gpu" else "none")
+                         device_type="none" if dev == "cpu" else "AMDGPU")
     gg = igg.get_global_grid()
     nd = 3 if nz > 1 else (2 if ny > 1 else 1)
     base = (nx, ny, nz)[:nd]
@@ -69,7 +74,7 @@ def scenario_gather(dev, dt):
     dtype = DTYPES[dt]
     nx, ny, nz = 4, 3, 2
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, quiet=True, select_device=False,
-                                                          device_type="AMDGPU" if dev == "gpu" else "none")
+                                                          device_type="none" if dev == "cpu" else "AMDGPU")
     for root in sorted({0, nprocs - 1}):
         for shape in [(nx,), (nx, ny), (nx, ny, nz)]:
             A = torch.full(shape, float(me + 1), dtype=dtype).to(device)
@@ -101,7 +106,7 @@ def scenario_diffusion(dev, nx, ny, nz, steps, overlap):
     device = _device(dev)
     nx, ny, nz, steps = int(nx), int(ny), int(nz), int(steps)
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, quiet=True, select_device=False,
-                                                          device_type="AMDGPU" if dev == "gpu" else "none")
+                                                          device_type="none" if dev == "cpu" else "AMDGPU")
     gg = igg.get_global_grid()
     v = os.environ.get("IGG_TEST_VARIANT")
     m = Diffusion3D(dtype=torch.float64, device=device, overlap=bool(int(overlap)),
@@ -134,7 +139,7 @@ def scenario_diffusion_fused(nx, ny, nz, steps, periodic, graph):
     arenas) vs stencil + update_halo_: bitwise equal T on every rank."""
     from igg.models.diffusion3d import Diffusion3D
 
-    device = _device("gpu")
+    device = _device(os.environ.get("IGG_TEST_DEV", "gpu"))
     nx, ny, nz, steps, per = int(nx), int(ny), int(nz), int(steps), int(periodic)
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, periodx=per, periody=per, periodz=per,
                                                           quiet=True, select_device=False)
@@ -175,7 +180,7 @@ def scenario_acoustic(dev, nx, ny, steps):
     device = _device(dev)
     nx, ny, steps = int(nx), int(ny), int(steps)
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, 1, quiet=True, select_device=False,
-                                                          device_type="AMDGPU" if dev == "gpu" else "none")
+                                                          device_type="none" if dev == "cpu" else "AMDGPU")
     gg = igg.get_global_grid()
     m = Acoustic2D(dtype=torch.float64, device=device)
     m.run(steps)
@@ -204,6 +209,7 @@ def scenario_acoustic(dev, nx, ny, steps):
 def scenario_gather_async():
     """gather_async_: root pulls every block (IPC + copy engine), the caller
     overlaps other work, wait() reorders; then A may change again."""
+    _device(os.environ.get("IGG_TEST_DEV", "gpu"))
     me, dims, nprocs, coords, comm = igg.init_global_grid(6, 5, 4, quiet=True, select_device=False,
                                                           device_type="AMDGPU")
     s = (6, 5, 4)
@@ -241,7 +247,7 @@ def scenario_fused_soak(nx, ny, nz, rounds, per_round):
 
     from igg.models.diffusion3d import Diffusion3D
 
-    device = _device("gpu")
+    device = _device(os.environ.get("IGG_TEST_DEV", "gpu"))
     nx, ny, nz, rounds, per_round = int(nx), int(ny), int(nz), int(rounds), int(per_round)
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, periodx=1, periody=1, periodz=1,
                                                           quiet=True, select_device=False)
@@ -283,7 +289,7 @@ def scenario_checkpoint(dev, model, tmpdir):
     is2d = model == "acoustic"
     me, dims, nprocs, coords, comm = igg.init_global_grid(18, 16, 1 if is2d else 14, periodx=1, quiet=True,
                                                           select_device=False,
-                                                          device_type="AMDGPU" if dev == "gpu" else "none")
+                                                          device_type="none" if dev == "cpu" else "AMDGPU")
     make = (lambda: Acoustic2D(dtype=torch.float64, device=device)) if is2d else \
         (lambda: Diffusion3D(dtype=torch.float64, device=device))
     a = make()
@@ -326,9 +332,18 @@ def scenario_put_timeout():
         except igg.IGGError as e:
             assert "timed out" in str(e)
         assert waited >= 1.0, waited
-        comm.mesh.clear_error()
     comm.barrier()
-    igg.finalize_global_grid()
+    if me == 0:
+        # The sticky error is reported by finalize, but only after every
+        # resource was released: the grid is reset and can be re-initialised.
+        try:
+            igg.finalize_global_grid()
+            raise AssertionError("expected finalize to report the put-transport timeout")
+        except igg.IGGError as e:
+            assert "timed out" in str(e)
+        assert not igg.grid_is_initialized()
+    else:
+        igg.finalize_global_grid()
     print(f"rank {me} put timeout OK")
 
 
@@ -365,7 +380,7 @@ def scenario_ring(dev):
     device = _device(dev)
     me, dims, nprocs, coords, comm = igg.init_global_grid(8, 4, 4, dimx=0, dimy=1, dimz=1, periodx=1, quiet=True,
                                                           select_device=False,
-                                                          device_type="AMDGPU" if dev == "gpu" else "none")
+                                                          device_type="none" if dev == "cpu" else "AMDGPU")
     gg = igg.get_global_grid()
     left, right = int(gg.neighbors[0, 0]), int(gg.neighbors[1, 0])
     send = torch.full((16,), float(me), dtype=torch.float64, device=device)
@@ -374,15 +389,76 @@ def scenario_ring(dev):
     recvs = [(recv.data_ptr() + 128, 128, right, 1), (recv.data_ptr(), 128, left, 0)]
     sends = [(send.data_ptr(), 128, left, 1), (send.data_ptr(), 128, right, 0)]
     fn = {"gloo": comm._gloo_p2p, "gloo-staged": comm._staged_p2p}.get(t.name)
-    if fn is None:
-        raise SystemExit(0)
-    fn(recvs, sends, dev == "gpu", torch.cuda.current_stream().cuda_stream if dev == "gpu" else 0)
-    if dev == "gpu":
+    stream = torch.cuda.current_stream().cuda_stream if dev != "cpu" else 0
+    if fn is not None:
+        fn(recvs, sends, dev != "cpu", stream)
+    elif t.name == "rccl":
+        # grouped ncclRecv/ncclSend: same-peer messages (2 ranks: left == right)
+        # match in issue order, like the reference's tagged MPI messages
+        t.p2p([r[:3] for r in recvs], [x[:3] for x in sends], stream)
+    else:
+        raise SystemExit(f"ring: transport {t.name!r} has no point-to-point interface")
+    if dev != "cpu":
         torch.cuda.synchronize()
     r = recv.cpu()
     assert (r[:16] == left).all() and (r[16:] == right).all(), f"rank {me}: ring wrong {r}"
     igg.finalize_global_grid()
     print(f"rank {me} ring OK")
+
+
+def scenario_barrier_timeout():
+    """Rank 1 never reaches the barrier: rank 0's bounded barrier
+    (IGG_COMM_TIMEOUT) raises IGGError naming the failure instead of hanging."""
+    import time
+
+    me, dims, nprocs, coords, comm = igg.init_global_grid(6, 5, 4, quiet=True, device_type="none")
+    comm.barrier()  # a healthy barrier first
+    if me == 0:
+        t0 = time.time()
+        try:
+            comm.barrier()
+            raise AssertionError("expected a barrier timeout")
+        except igg.IGGError as e:
+            assert "IGG_COMM_TIMEOUT" in str(e), str(e)
+        waited = time.time() - t0
+        assert 1.5 <= waited < 30, waited
+        assert comm.aborted
+    else:
+        time.sleep(float(os.environ["IGG_COMM_TIMEOUT"]) + 4)
+    print(f"rank {me} barrier timeout OK", flush=True)
+    os._exit(0)  # the process group is broken by design: skip finalize
+
+
+def scenario_collectives(dev):
+    """comm_cart interop: tensor all-reduce / broadcast and a scalar residual."""
+    device = _device(dev)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(6, 5, 4, quiet=True, select_device=False,
+                                                          device_type="AMDGPU" if dev != "cpu" else "none")
+    n = nprocs
+    for dtype in (torch.float64, torch.float32, torch.int32):
+        t = torch.full((5,), me + 1, dtype=dtype, device=device)
+        assert comm.allreduce_(t, "sum") is t
+        assert (t.cpu() == n * (n + 1) // 2).all(), t
+        for op, want in (("max", n), ("min", 1), ("prod", __import__("math").factorial(n))):
+            t = torch.full((3,), me + 1, dtype=dtype, device=device)
+            comm.allreduce_(t, op)
+            assert (t.cpu() == want).all(), (op, t)
+    for root in sorted({0, n - 1}):
+        t = torch.arange(7, dtype=torch.float64, device=device) * (me + 1)
+        comm.bcast_(t, root=root)
+        assert torch.equal(t.cpu(), torch.arange(7, dtype=torch.float64) * (root + 1)), (root, t)
+    r = comm.allreduce(float(me), "max")
+    assert r == float(n - 1), r
+    try:
+        comm.allreduce_(torch.zeros(1), "mean")
+        raise AssertionError("expected IGGError for an unknown op")
+    except igg.IGGError:
+        pass
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    igg.finalize_global_grid()
+    print(f"rank {me} collectives OK")
+
 
 
 if __name__ == "__main__":

@@ -1,0 +1,51 @@
+"""bench.py contract: ``--gpus N`` without a launcher starts N ranks itself and
+reports n_gpus == N; a --gpus/WORLD_SIZE mismatch or a failing rank is an error,
+never a silent 1-process number. Runs the CPU (gloo) plumbing mode."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", IGG_HOST_THREADS="2", **kw)
+    return env
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_self_launch_reports_n_gpus(n):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--device", "cpu", "--n", "24", "--steps", "4",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=150, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["steps"] == 4 and rec["warmup"] == 1
+    assert rec["config"]["self_launched"] is True
+    assert rec["config"]["finite"] is True
+    # whole-job aggregate = n x per-GPU T_eff
+    assert abs(rec["value"] - n * rec["config"]["t_eff_per_gpu_GBs"]) <= 1e-3 * rec["value"] + 0.01
+    assert rec["ms_per_step"] == rec["config"]["t_it_ms"]
+
+
+def test_world_size_mismatch_is_an_error():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--n", "16", "--steps", "1",
+                        "--warmup", "0"], capture_output=True, text=True, timeout=60,
+                       env=_env(WORLD_SIZE="1", RANK="0"), cwd=ROOT)
+    assert r.returncode != 0
+    assert "refusing" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+def test_failing_rank_fails_the_launch():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--n", "1", "--steps", "1",
+                        "--warmup", "0"], capture_output=True, text=True, timeout=120, env=_env(), cwd=ROOT)
+    assert r.returncode != 0
+    assert "self-launch" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())

@@ -43,6 +43,21 @@ def test_mismatched_grid_is_refused(tmp_path):
     igg.finalize_global_grid(finalize_MPI=False)
 
 
+def test_stale_block_from_another_save_is_refused(tmp_path):
+    """A block file left from an earlier save (e.g. a rank crashed before
+    rewriting it) must not be mixed with a manifest naming a later step."""
+    from safetensors.torch import save_file
+
+    prefix = str(tmp_path / "c")
+    igg.init_global_grid(10, 8, 6, quiet=True, init_MPI=False, device_type="none")
+    A = torch.zeros(10, 8, 6)
+    path = igg.save_checkpoint(prefix, step=3, A=A)
+    save_file({"A": A}, path, metadata={"coords": "[0, 0, 0]", "step": "2"})  # the stale block
+    with pytest.raises(igg.IGGError, match="step 2"):
+        igg.load_checkpoint(prefix)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
 def test_model_restore_checks_shapes(tmp_path):
     prefix = str(tmp_path / "c")
     igg.init_global_grid(10, 8, 6, quiet=True, init_MPI=False, device_type="none")

@@ -363,3 +363,61 @@ def test_gpu_overlap_capture(gpu, monkeypatch, transport):
     torch.cuda.synchronize()
     assert torch.equal(a.T, b.T)
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_gpu_auto_mode_picks_the_timed_winner(gpu):
+    """'auto' times sequential vs one-phase on the first eager exchange of a
+    field set that reaches other ranks (here: the RCCL loopback) and keeps the
+    faster for that field set; results stay bitwise."""
+    from igg.parallel import halo as H
+
+    n = (40, 36, 32)
+    igg.init_global_grid(*n, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    H.enable_loopback()
+    assert H.halo_mode() == "auto"
+    before = len(H.tuned_modes())
+    A = encode(torch.zeros(*n, dtype=torch.float64))
+    ref = A.clone()
+    Ag = zero_boundaries(A.clone()).to(gpu)
+    igg.update_halo_(Ag)
+    assert torch.equal(Ag.cpu(), ref)
+    log = H.tuned_modes()
+    assert len(log) == before + 1
+    times, win = log[-1]
+    assert set(times) == {"sequential", "onephase"}
+    assert win == min(times, key=times.get)
+    assert H.plan_mode(Ag) == win
+    igg.update_halo_(Ag)  # cached: no second measurement
+    assert len(H.tuned_modes()) == before + 1
+    H.set_halo_mode("onephase")  # an explicit mode wins over the measurement
+    assert H.plan_mode(Ag) == "onephase"
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+def test_gpu_bounded_sync_raises_instead_of_hanging(gpu):
+    """A kernel that does not finish (stand-in: a 4 s spin, like an RCCL kernel
+    waiting on a dead peer) makes the bounded device wait raise after its
+    timeout instead of blocking; once the kernel ends the GPU drains normally."""
+    import time
+
+    from igg import native
+    from igg.parallel.comm import bounded_device_sync
+
+    s = torch.cuda.Stream()
+    native.gpu_spin(4.0, s.cuda_stream)
+    t0 = time.time()
+    with pytest.raises(igg.IGGError, match="did not drain"):
+        bounded_device_sync(timeout=1.0, what="test")
+    assert 0.9 <= time.time() - t0 < 3.5
+    bounded_device_sync(timeout=30.0, what="test")
+    assert time.time() - t0 >= 3.5
+
+
+def test_gpu_tensor_collectives_single_rank(gpu):
+    igg.init_global_grid(6, 5, 4, quiet=True, init_MPI=False)
+    comm = igg.get_global_grid().comm
+    t = torch.arange(4, dtype=torch.float64, device=gpu)
+    assert torch.equal(comm.allreduce_(t, "sum").cpu(), torch.arange(4, dtype=torch.float64))
+    assert torch.equal(comm.bcast_(t, 0).cpu(), torch.arange(4, dtype=torch.float64))
+    assert comm.allreduce(3.5, "max") == 3.5
+    igg.finalize_global_grid(finalize_MPI=False)

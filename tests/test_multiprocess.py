@@ -126,3 +126,13 @@ def test_fused_soak_with_rank_skew(nprocs, kernel):
     ranks stay bitwise equal to stencil + update_halo_."""
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "30", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
     run_ranks(nprocs, "fused_soak", 20, 18, 32, 60, 40, env_extra=env, timeout=170)
+
+
+# --- failure path and comm_cart interop ------------------------------------
+def test_barrier_timeout_raises_instead_of_hanging():
+    run_ranks(2, "barrier_timeout", env_extra={"IGG_COMM_TIMEOUT": "3"}, timeout=60)
+
+
+@pytest.mark.parametrize("nprocs", [2, 4])
+def test_tensor_collectives_cpu(nprocs):
+    run_ranks(nprocs, "collectives", "cpu")
