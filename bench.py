@@ -306,10 +306,14 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
     cands = [(name, t, mode, False) for name, t, mode in TRANSPORT_CANDIDATES if valid.get(name) == "ok"]
     # Overlap (boundary planes first, exchange on a second stream next to the
     # interior) only pays without z-neighbours: x/y boundary planes are cheap
-    # rows, z-planes of a C-ordered field are maximally strided. RCCL's p2p
-    # kernels stall next to a full-GPU stencil, so only put is tried overlapped.
-    if valid.get("put") == "ok" and getattr(model, "can_overlap", False) and not any(model.sides[2]):
-        cands.append(("put+overlap", "put", "auto", True))
+    # rows, z-planes of a C-ordered field are maximally strided. (RCCL's p2p
+    # kernels next to a full-GPU stencil measured slower than serial in
+    # loopback, profiles/r1_ctas/; over real xGMI the A/B decides.)
+    if getattr(model, "can_overlap", False) and not any(model.sides[2]):
+        if valid.get("put") == "ok":
+            cands.append(("put+overlap", "put", "auto", True))
+        if valid.get("rccl-sequential") == "ok":
+            cands.append(("rccl+overlap", "rccl", "sequential", True))
     if not cands:
         raise RuntimeError("no device transport passed the bitwise validation against the host-staged path")
     times = {}

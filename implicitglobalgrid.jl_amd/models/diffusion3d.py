@@ -12,6 +12,9 @@ MI355X design of a time step (``overlap=True`` and at least one neighbour):
       sends) -> update_halo_(T2)  [pack -> RCCL -> unpack, x->y->z]
   compute stream:              interior of T2 (everything else)
   join, swap T <-> T2.
+  (With the RCCL transport the exchange stays on the issuing stream and the
+  interior goes to the forked one: RCCL captured on a forked stream crashes
+  hipGraph capture, benchmarks/rccl_capture_repro.py.)
 
 Both read T only; they write disjoint parts of T2, so the exchange hides behind
 the interior update. Without neighbours (1 GPU, non-periodic) the step is one
@@ -41,6 +44,12 @@ from ..utils.tools import coords_g, nx_g, ny_g, nz_g
 # Time steps per captured hipGraph (even): one replay launch (~9 us) per
 # GRAPH_STEPS steps instead of per 2 (profiles/r1_fused/graph_gaps.txt).
 GRAPH_STEPS = 10
+
+
+def _rccl_transport() -> bool:
+    from ..parallel import halo as H
+
+    return H.transport_name() == "rccl"
 
 
 class Diffusion3D:
@@ -263,16 +272,31 @@ class Diffusion3D:
             hs = self.halo_stream
             cs = self.compute_stream or main
             stencil.diffusion3d_(T2, T, Cp, boxes=self.slabs, **self._kw(self.halo_variant, self.halo_rounds))
-            hs.wait_stream(main)
-            if cs is not main:
-                cs.wait_stream(main)
-            with torch.cuda.stream(hs):
+            if _rccl_transport():
+                # RCCL's p2p group must run on the stream the step was issued
+                # on: captured on a stream forked from the capture origin it
+                # crashes hipGraph capture (RCCL 2.26, SIGSEGV at the end of
+                # the capture); on the origin, with the interior on a forked
+                # stream running concurrently, it captures and replays
+                # (benchmarks/rccl_capture_repro.py, profiles/r2_rccl_capture/).
+                # So the roles swap: interior on the side stream, exchange here.
+                side = cs if cs is not main else hs
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw(None, self.interior_rounds))
                 update_halo_(T2)
-            with torch.cuda.stream(cs):
-                stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw(None, self.interior_rounds))
-            main.wait_stream(hs)
-            if cs is not main:
-                main.wait_stream(cs)
+                main.wait_stream(side)
+            else:
+                hs.wait_stream(main)
+                if cs is not main:
+                    cs.wait_stream(main)
+                with torch.cuda.stream(hs):
+                    update_halo_(T2)
+                with torch.cuda.stream(cs):
+                    stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw(None, self.interior_rounds))
+                main.wait_stream(hs)
+                if cs is not main:
+                    main.wait_stream(cs)
         elif self.timer is not None:
             with self.timer.phase("stencil"):
                 stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
@@ -302,15 +326,6 @@ class Diffusion3D:
             raise ValueError("Diffusion3D.capture: steps must be even and >= 2")
         if self.device.type != "cuda":
             raise RuntimeError("Diffusion3D.capture: hipGraphs need a GPU model")
-        if self.overlap and not self.fused:
-            from ..parallel import halo as H
-
-            if H.transport_name() == "rccl":
-                # Capturing RCCL on the forked halo stream of the overlapped
-                # step crashed the process in RCCL 2.26 (profiles/r1_ctas/):
-                # refuse loudly; run() then steps eagerly.
-                raise RuntimeError("Diffusion3D.capture: the overlapped step with the RCCL transport "
-                                   "cannot be captured; use the serial step, the put transport or eager steps")
         if not self._warm:
             self.step()
         if self.fused and not self._fprimed:
