@@ -470,6 +470,9 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
         py::arg("stream") = 0, py::arg("rounds") = 0);
   m.def("diffusion3d_fused_variant_ok", &diffusion3d_fused_variant_ok);
+  m.def("fused_debug", [](uintptr_t stamps, int force_sel) {
+    fused_debug(reinterpret_cast<int64_t*>(stamps), force_sel);
+  }, py::arg("stamps"), py::arg("force_sel") = -1);
   py::class_<FusedHalo, std::shared_ptr<FusedHalo>>(m, "FusedHalo")
       .def(py::init([](std::shared_ptr<PeerMesh> mesh, const Int3& n, int elem_bytes,
                        const std::array<std::array<int, 2>, 3>& nb) {

@@ -59,6 +59,11 @@ struct HaloIOArgs {
   int64_t zpitch;
 };
 bool diffusion3d_fused_variant_ok(int v);
+// Diagnostics of the fused kernel: per-wave {feature class, start, end, hw id}
+// stamps (4 x int64 per wave, wall_clock64 ticks) into device memory `stamps`
+// (nullptr: off), and force_sel >= 0 runs every wave with that feature class
+// (-1: per-wave choice). Applies to subsequent fused launches.
+void fused_debug(int64_t* stamps, int force_sel);
 // Inner-box update through the fused kernel without exchange features
 // (tiling = a fused-capable variant index); used by the "hx" variants.
 void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t stream);

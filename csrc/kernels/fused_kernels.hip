@@ -52,25 +52,41 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
+// Block chunk index in march order (chunks holding the x send planes first).
+__device__ __forceinline__ int64_t hx_chunk(int64_t cxr, int64_t nch) {
+  return (cxr == 0 || nch < 2) ? cxr : (cxr == 1 ? nch - 1 : cxr - 1);
+}
+
 template <typename T>
 struct HxScal {
   int64_t n0, n1, n2, zp;
   int64_t ntz, nty, ch;  // z tiles, y tiles, planes per chunk
   T rdx2, rdy2, rdz2, dtlam;
+  // Diagnostics (fused_debug): per-wave {class, start, end, cu} stamps
+  // (wall_clock64 ticks) into `stamps` (4 int64 per wave) when non-null;
+  // force_sel >= 0 runs every wave with that feature class.
+  int64_t* stamps;
+  int force_sel;
 };
+
+// Diagnostics state set by fused_debug() and copied into the next launches.
+int64_t* g_hx_stamps = nullptr;
+int g_hx_force_sel = -1;
 
 // FEAT bits (compile-time exchange features): 1 x-in, 2 y-in, 4 z-in, 8 z-out,
 // 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants); 512 =
-// lane-distributed z-segment edge loads (plain variants, below). 207 = the full
+// lane-distributed z-segment edge loads (plain variants, below); 1024 = one
+// workgroup per CU (launch); 2048 = no per-wave specialisation (kernel below);
+// 4096 = z edge values staged through LDS instead of v_readlane. 207 = the full
 // exchange, 0 = the plain update (variants 21+); other subsets served the cost
 // bisect (profiles/r1_fused/feature_bisect_*).
-template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
-__global__ void __launch_bounds__(64 * BY * BZ)
-diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
-                      const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
-                      const T* __restrict__ yi1, const T* __restrict__ zi0, const T* __restrict__ zi1,
-                      T* __restrict__ xo0, T* __restrict__ xo1, T* __restrict__ yo0, T* __restrict__ yo1,
-                      T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T> a) {
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT>
+__device__ __forceinline__ void
+hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
+         const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
+         const T* __restrict__ yi1, const T* __restrict__ zi0, const T* __restrict__ zi1,
+         T* __restrict__ xo0, T* __restrict__ xo1, T* __restrict__ yo0, T* __restrict__ yo1,
+         T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T>& a) {
   using V = typename Vec<T, VZ>::type;
   constexpr int W = 64 * VZ * BZ;
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -83,7 +99,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   // instead of at the kernel's tail. Scheduling only: results are unchanged.
   const int64_t nch = (a.n0 - 2 + a.ch - 1) / a.ch;
   const int64_t cxr = rest / a.nty;
-  const int64_t cx = (cxr == 0 || nch < 2) ? cxr : (cxr == 1 ? nch - 1 : cxr - 1);
+  const int64_t cx = hx_chunk(cxr, nch);
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wz = wid % BZ, wy = wid / BZ;
@@ -150,6 +166,15 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   const bool remote = zout || yrow0 || yrow1 || (xs == 1 && xo0) || (xe == n0 - 1 && xo1);
   T znext = T(0), zv = T(0);
   if (zsrc) znext = zsrc[xs * a.zp];
+  // FEAT 4096: the z edge values move between the edge lane and the
+  // lane-distributed row layout through 4*RY LDS slots of this wave (in/out x
+  // lo/hi) instead of v_readlane (whose SGPR result feeds VALU with wait states
+  // that one wave per SIMD cannot hide: profiles/r2_fused_spec/).
+  T* zs = nullptr;
+  if constexpr ((FEAT & 4096) != 0) {
+    __shared__ T zslots[BY * BZ * 4 * RY];
+    zs = zslots + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (4 * RY);
+  }
   // Deferred sends (DF): the y row / z values of step x leave after the loads
   // of step x+1 were issued, so their acknowledgement never gates those loads.
   V ysend;
@@ -193,15 +218,31 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     if (zin) {
       const T zcur = znext;
       if (zsrc && x + 1 < xe) znext = zsrc[(x + 1) * a.zp];
+      if constexpr ((FEAT & 4096) != 0) {
+        // through the wave's LDS slots: no v_readlane -> SGPR -> VALU chain
+        if (lo_l || hi_l) zs[(lane < 32 ? 0 : RY) + rl] = zcur;
 #pragma unroll
-      for (int r = 0; r < RY; ++r) {
-        if (zin_lo) {
-          const T v = lane_read(zcur, r);
-          if (lane == 0) tc[r][0] = v;
+        for (int r = 0; r < RY; ++r) {
+          if (zin_lo) {
+            const T v = zs[r];
+            if (lane == 0) tc[r][0] = v;
+          }
+          if (zin_hi) {
+            const T v = zs[RY + r];
+            if (lane == zh) tc[r][VZ - 1] = v;
+          }
         }
-        if (zin_hi) {
-          const T v = lane_read(zcur, 32 + r);
-          if (lane == zh) tc[r][VZ - 1] = v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < RY; ++r) {
+          if (zin_lo) {
+            const T v = lane_read(zcur, r);
+            if (lane == 0) tc[r][0] = v;
+          }
+          if (zin_hi) {
+            const T v = lane_read(zcur, 32 + r);
+            if (lane == zh) tc[r][VZ - 1] = v;
+          }
         }
       }
     }
@@ -280,15 +321,23 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
           if (DF && !yrow0) { ysend = out; ysend_dst = zown ? yrow1 + x * n2 + zl : nullptr; }
           else if (zown) *reinterpret_cast<V*>(yrow1 + x * n2 + zl) = out;
         }
-        if (zout_lo) {
-          const T v = lane_read(out[1], 0);
-          if (lane == r) zv = v;
-        }
-        if (zout_hi) {
-          const T v = lane_read(out[VZ - 2], zh);
-          if (lane == 32 + r) zv = v;
+        if constexpr ((FEAT & 4096) != 0) {
+          if (zout_lo && lane == 0) zs[2 * RY + r] = out[1];
+          if (zout_hi && lane == zh) zs[3 * RY + r] = out[VZ - 2];
+        } else {
+          if (zout_lo) {
+            const T v = lane_read(out[1], 0);
+            if (lane == r) zv = v;
+          }
+          if (zout_hi) {
+            const T v = lane_read(out[VZ - 2], zh);
+            if (lane == 32 + r) zv = v;
+          }
         }
       }
+    }
+    if constexpr ((FEAT & 4096) != 0) {
+      if (zdst) zv = zs[(lane < 32 ? 2 * RY : 3 * RY) + rl];
     }
     if (zdst) {
       if (DF) zsend_dst = zdst + x * a.zp;
@@ -319,6 +368,76 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   // Remote stores acknowledged before the wave retires (the sync kernel that
   // publishes the arrival flags runs after this kernel on the same stream).
   if (remote) __builtin_amdgcn_s_waitcnt(0);
+}
+
+// The kernel: each wave runs the sweep specialised to the exchange features its
+// tile actually touches. A wave away from every exchanged face (most of them:
+// not in the first/last x chunk, not in the first/last y row of tiles, not in a
+// z-edge tile) runs the plain sweep (FEAT without exchange bits): the exchange
+// code only present in the same loop, with its pointers null at run time,
+// measured +60-70 us per step for tilings 11/40 (profiles/r2_fused_spec/),
+// because it changes the hot loop's schedule. The test is wave-uniform, so the
+// dispatch is a scalar branch; results are unchanged (the skipped features are
+// no-ops for such a wave).
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
+__global__ void __launch_bounds__(64 * BY * BZ)
+diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
+                      const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
+                      const T* __restrict__ yi1, const T* __restrict__ zi0, const T* __restrict__ zi1,
+                      T* __restrict__ xo0, T* __restrict__ xo1, T* __restrict__ yo0, T* __restrict__ yo1,
+                      T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T> a) {
+  constexpr int FX = FEAT & (1 | 64), FY = FEAT & (2 | 128), FZ = FEAT & (4 | 8);
+  constexpr int FK = FEAT & ~(1 | 2 | 4 | 8 | 64 | 128);
+#define IGG_HX_SWEEP(F)                                                                                  \
+  hx_sweep<T, BY, RY, VZ, PF, BZ, DF, (F)>(t2, t, cpp, xi0, xi1, yi0, yi1, zi0, zi1, xo0, xo1, yo0, yo1, \
+                                           zo0, zo1, a)
+  if constexpr ((FX | FY | FZ) == 0 || (FEAT & 2048) != 0) {
+    IGG_HX_SWEEP(FEAT);  // nothing to specialise, or specialisation disabled (FEAT 2048)
+  } else {
+    constexpr int W = 64 * VZ * BZ;
+    const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t rest = b / a.ntz;
+    const int64_t tz = b % a.ntz, ty = rest % a.nty;
+    const int64_t n0 = a.n0, n1 = a.n1, n2 = a.n2;
+    const int64_t nch = (n0 - 2 + a.ch - 1) / a.ch;
+    const int64_t cx = hx_chunk(rest / a.nty, nch);
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wz = wid % BZ, wy = wid / BZ;
+    const int64_t zt = tz * W + wz * (64 * VZ);
+    const int64_t y0 = 1 + ty * (BY * RY) + wy * RY;
+    const int64_t xs = 1 + cx * a.ch;
+    const int64_t xe = min(xs + a.ch, n0 - 1);
+    const int64_t nv = min<int64_t>(RY, n1 - 1 - y0);
+    // conservative: a chunk that reads plane 0 / n0-1 or computes plane 1 / n0-2
+    const bool wx = FX != 0 && (xs <= 1 || xe >= n0 - 2);
+    const bool wyy = FY != 0 && (y0 <= 1 || y0 + nv >= n1 - 1);
+    const bool wzz = FZ != 0 && (zt == 0 || (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ));
+    int sel = __builtin_amdgcn_readfirstlane((wx ? 1 : 0) | (wyy ? 2 : 0) | (wzz ? 4 : 0));
+    if (a.force_sel >= 0) sel = a.force_sel;
+    const int64_t t_start = a.stamps ? wall_clock64() : 0;
+    switch (sel) {
+      case 0: IGG_HX_SWEEP(FK); break;
+      case 1: IGG_HX_SWEEP(FK | FX); break;
+      case 2: IGG_HX_SWEEP(FK | FY); break;
+      case 3: IGG_HX_SWEEP(FK | FX | FY); break;
+      case 4: IGG_HX_SWEEP(FK | FZ); break;
+      case 5: IGG_HX_SWEEP(FK | FX | FZ); break;
+      case 6: IGG_HX_SWEEP(FK | FY | FZ); break;
+      default: IGG_HX_SWEEP(FEAT); break;
+    }
+    if (a.stamps) {
+      // one vector store per wave (lane 0; lane-dependent address -> VGPR store)
+      const int lane = threadIdx.x & 63;
+      const int64_t w = (static_cast<int64_t>(blockIdx.x) * (BY * BZ) + wid) * 4;
+      if (lane < 4) {
+        int cu = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(cu));
+        const int64_t v[4] = {sel, t_start, wall_clock64(), static_cast<int64_t>(cu)};
+        a.stamps[w + lane] = v[lane];
+      }
+    }
+  }
+#undef IGG_HX_SWEEP
 }
 
 int resident(const void* kernel, int block, size_t lds = 0) {
@@ -361,6 +480,8 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
   a.rdy2 = static_cast<T>(d.rd2[1]);
   a.rdz2 = static_cast<T>(d.rd2[2]);
   a.dtlam = static_cast<T>(d.dt_lam);
+  a.stamps = g_hx_stamps;
+  a.force_sel = g_hx_force_sel;
   auto in = [&](int k, int s) { return reinterpret_cast<const T*>(io.in[k][s]); };
   auto out = [&](int k, int s) { return reinterpret_cast<T*>(io.out[k][s]); };
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(block), lds, stream,
@@ -408,6 +529,10 @@ void dispatch(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hip
     case 14: launch_mode<T, 2, 8, 4, false, 2>(d, io, mode, s); break;
     case 40: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024>(d, io, mode, s); break;
     case 50: launch_mode<T, 4, 4, 4, false, 1, 1024>(d, io, mode, s); break;  // tiling 0, one WG per CU
+    // + z edge through LDS (FEAT 4096): tiling 11 zl occ1 / tiling 0 occ1 / tiling 0
+    case 41: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024 | 4096>(d, io, mode, s); break;
+    case 51: launch_mode<T, 4, 4, 4, false, 1, 1024 | 4096>(d, io, mode, s); break;
+    case 52: launch_mode<T, 4, 4, 4, false, 1, 4096>(d, io, mode, s); break;
     default: fail("diffusion3d (fused halo): variant ", v, " has no fused instantiation");
   }
 }
@@ -455,8 +580,13 @@ void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t
   else fail("diffusion3d: only float32/float64 are supported");
 }
 
+void fused_debug(int64_t* stamps, int force_sel) {
+  g_hx_stamps = stamps;
+  g_hx_force_sel = force_sel;
+}
+
 bool diffusion3d_fused_variant_ok(int v) {
-  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14 || v == 40 || v == 50;
+  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14 || v == 40 || v == 41 || v == 50 || v == 51 || v == 52;
 }
 
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
