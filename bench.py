@@ -54,8 +54,12 @@ import time
 # (Fused variant 40 - tiling 11 with lane-distributed z-segment edge loads at
 # one workgroup per CU, no register spill - measured 0.65-0.75 ms in every
 # loopback topology, slower than these: profiles/r1_zl/.)
+# Round 2: the fused kernel runs each wave with only the exchange features its
+# tile touches (profiles/r2_fused_spec/), so variant 40 (the fastest plain
+# tiling) is exchange-free away from the exchanged faces and joins the A/B;
+# tiling 11's z-compiled-out modes (superseded by that) left it.
 FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3),
-                    (11, 2, 2), (11, 3, 2), (50, 0, 2), (50, 1, 2), (50, 1, 4))
+                    (40, 0, 2), (40, 1, 2), (50, 0, 2), (50, 1, 2), (50, 1, 3))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")

@@ -409,9 +409,12 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     const int64_t xe = min(xs + a.ch, n0 - 1);
     const int64_t nv = min<int64_t>(RY, n1 - 1 - y0);
     // conservative: a chunk that reads plane 0 / n0-1 or computes plane 1 / n0-2
-    const bool wx = FX != 0 && (xs <= 1 || xe >= n0 - 2);
-    const bool wyy = FY != 0 && (y0 <= 1 || y0 + nv >= n1 - 1);
-    const bool wzz = FZ != 0 && (zt == 0 || (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ));
+    // Per side, and only sides with a neighbour count (a 2x1x1 rank runs no
+    // y/z code at all; a 2x2x2 corner rank only the z-edge tiles of one side).
+    const bool wx = FX != 0 && ((xs <= 1 && (xi0 || xo0)) || (xe >= n0 - 2 && (xi1 || xo1)));
+    const bool wyy = FY != 0 && ((y0 <= 1 && (yi0 || yo0)) || (y0 + nv >= n1 - 1 && (yi1 || yo1)));
+    const bool wzz = FZ != 0 && ((zt == 0 && (zi0 || zo0)) ||
+                                 (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ && (zi1 || zo1)));
     int sel = __builtin_amdgcn_readfirstlane((wx ? 1 : 0) | (wyy ? 2 : 0) | (wzz ? 4 : 0));
     if (a.force_sel >= 0) sel = a.force_sel;
     const int64_t t_start = a.stamps ? wall_clock64() : 0;
