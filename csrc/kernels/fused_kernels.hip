@@ -161,11 +161,16 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   // Lane-distributed z values: row r of the low edge in lane r, of the high
   // edge in lane 32+r (rows < nv).
   const bool lo_l = lane < 32 && rl < nv, hi_l = lane >= 32 && rl < nv;
-  const T* zsrc = lo_l && zin_lo ? zi0 + (y0 - 1) + rl : (hi_l && zin_hi ? zi1 + (y0 - 1) + rl : nullptr);
+  // Every lane loads (lanes without a row of their own read a valid dummy in
+  // the same region): a load under a per-lane condition would be a divergent
+  // branch around a load in the hot loop, which costs the loop its prefetch.
+  const T* zsrc = lo_l && zin_lo ? zi0 + (y0 - 1) + rl
+                                 : (hi_l && zin_hi ? zi1 + (y0 - 1) + rl
+                                                   : (zin_lo ? zi0 : zi1) + (y0 - 1));
   T* zdst = lo_l && zout_lo ? zo0 + (y0 - 1) + rl : (hi_l && zout_hi ? zo1 + (y0 - 1) + rl : nullptr);
   const bool remote = zout || yrow0 || yrow1 || (xs == 1 && xo0) || (xe == n0 - 1 && xo1);
   T znext = T(0), zv = T(0);
-  if (zsrc) znext = zsrc[xs * a.zp];
+  if (zin) znext = zsrc[xs * a.zp];
   // FEAT 4096: the z edge values move between the edge lane and the
   // lane-distributed row layout through 4*RY LDS slots of this wave (in/out x
   // lo/hi) instead of v_readlane (whose SGPR result feeds VALU with wait states
@@ -217,7 +222,7 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     // tiling: profiles/r1_fused/feature_bisect_v11_zin_alt.log.)
     if (zin) {
       const T zcur = znext;
-      if (zsrc && x + 1 < xe) znext = zsrc[(x + 1) * a.zp];
+      if (x + 1 < xe) znext = zsrc[(x + 1) * a.zp];
       if constexpr ((FEAT & 4096) != 0) {
         // through the wave's LDS slots: no v_readlane -> SGPR -> VALU chain
         if (lo_l || hi_l) zs[(lane < 32 ? 0 : RY) + rl] = zcur;
@@ -233,16 +238,15 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
           }
         }
       } else {
+        // Branch-free: per-row uniform branches split the loop body into
+        // basic blocks the scheduler cannot interleave across, which at one
+        // wave per SIMD serialises the rows (profiles/r2_fused_spec/).
+        const bool pl = zin_lo && lane == 0, ph = zin_hi && lane == zh;
 #pragma unroll
         for (int r = 0; r < RY; ++r) {
-          if (zin_lo) {
-            const T v = lane_read(zcur, r);
-            if (lane == 0) tc[r][0] = v;
-          }
-          if (zin_hi) {
-            const T v = lane_read(zcur, 32 + r);
-            if (lane == zh) tc[r][VZ - 1] = v;
-          }
+          const T vl = lane_read(zcur, r), vh = lane_read(zcur, 32 + r);
+          tc[r][0] = pl ? vl : tc[r][0];
+          tc[r][VZ - 1] = ph ? vh : tc[r][VZ - 1];
         }
       }
     }
@@ -324,15 +328,11 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         if constexpr ((FEAT & 4096) != 0) {
           if (zout_lo && lane == 0) zs[2 * RY + r] = out[1];
           if (zout_hi && lane == zh) zs[3 * RY + r] = out[VZ - 2];
-        } else {
-          if (zout_lo) {
-            const T v = lane_read(out[1], 0);
-            if (lane == r) zv = v;
-          }
-          if (zout_hi) {
-            const T v = lane_read(out[VZ - 2], zh);
-            if (lane == 32 + r) zv = v;
-          }
+        } else if constexpr ((FEAT & 8) != 0) {
+          // branch-free (see the z-in patch): unconditional readlanes + selects
+          const T vl = lane_read(out[1], 0), vh = lane_read(out[VZ - 2], zh);
+          zv = (zout_lo && lane == r) ? vl : zv;
+          zv = (zout_hi && lane == 32 + r) ? vh : zv;
         }
       }
     }
