@@ -30,10 +30,13 @@ def main():
     igg.tic()
     model.run(a.nt)
     t = igg.toc()
+    # Global maximum over the ranks through the grid's communicator (the
+    # reference apps call MPI.Allreduce on comm_cart for such diagnostics).
+    t_max = comm.allreduce_(model.T.max().reshape(1).clone(), "max")
     if me == 0:
         t_it = t / a.nt
         print(f"{nprocs} process(es) {dims.tolist()}: {t:.3f} s, {t_it * 1e3:.3f} ms/step, "
-              f"T_eff = {t_eff_gbs(model, t_it):.2f} GB/s per process, T_max = {float(model.T.max()):.6f}")
+              f"T_eff = {t_eff_gbs(model, t_it):.2f} GB/s per process, global T_max = {float(t_max):.6f}")
     igg.finalize_global_grid()
 
 

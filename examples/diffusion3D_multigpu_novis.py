@@ -40,10 +40,12 @@ def main():
     t = igg.toc()
     model.sync_halo()                                                        # halos of T valid again (fused mode)
     model.close()
+    t_max = comm.allreduce_(model.T.max().reshape(1).clone(), "max")        # global max (RCCL, on the stream)
     if me == 0:
         t_it = t / a.nt
         print(f"{nprocs} process(es) {dims.tolist()}, local {a.nx}^3, global {igg.nx_g()}x{igg.ny_g()}x{igg.nz_g()}: "
-              f"{t:.3f} s, {t_it * 1e3:.4f} ms/step, T_eff = {t_eff_gbs(model, t_it):.1f} GB/s per GPU")
+              f"{t:.3f} s, {t_it * 1e3:.4f} ms/step, T_eff = {t_eff_gbs(model, t_it):.1f} GB/s per GPU, "
+              f"global T_max = {float(t_max):.6f}")
     igg.finalize_global_grid()                                               # Finalize the implicit global grid
 
 
