@@ -406,12 +406,10 @@ PYBIND11_MODULE(_igg_native, m) {
              return std::make_unique<PullGatherer>(rank, nranks, ag);
            }),
            py::arg("rank"), py::arg("nranks"), py::arg("allgather"))
-      .def("start", [](PullGatherer& g, const FieldTuple& a, int root, const Int3& dims) {
-        g.start(to_field(a), root, dims);
-      })
-      .def("wait", [](PullGatherer& g, uintptr_t dst, uintptr_t s) {
-        g.wait(reinterpret_cast<void*>(dst), as_stream(s));
-      })
+      .def("start", [](PullGatherer& g, const FieldTuple& a, uintptr_t dst, int root, const Int3& dims,
+                       uintptr_t s) { g.start(to_field(a), reinterpret_cast<void*>(dst), root, dims, as_stream(s)); },
+           py::arg("a"), py::arg("dst"), py::arg("root"), py::arg("dims"), py::arg("stream"))
+      .def("wait", [](PullGatherer& g, uintptr_t s) { g.wait(as_stream(s)); }, py::arg("stream"))
       .def_property_readonly("pending", &PullGatherer::pending)
       .def("free", &PullGatherer::free);
   m.def("gather_reorder", [](uintptr_t src, uintptr_t dst, const Int3& s, const Int3& dims,

@@ -51,44 +51,79 @@ void Gatherer::gather(const Field& a, void* dst, int root, const Int3& dims, Rcc
 
 // ------------------------------------------------------------ PullGatherer
 
+namespace {
+
+constexpr int MAX_COPY_STREAMS = 8;
+
+// One 3-D copy of a C-contiguous block of extent s (elements) into its place
+// (block coords c) in the C-contiguous global array of extent dims*s.
+void copy_block(const void* src, void* dst, const Int3& s, const Int3& dims, const Int3& c, int eb,
+                hipStream_t stream) {
+  const size_t row = static_cast<size_t>(s[2]) * eb;
+  hipMemcpy3DParms p{};
+  p.srcPtr = make_hipPitchedPtr(const_cast<void*>(src), row, row, static_cast<size_t>(s[1]));
+  p.dstPtr = make_hipPitchedPtr(dst, static_cast<size_t>(dims[2] * s[2]) * eb, static_cast<size_t>(dims[2] * s[2]) * eb,
+                                static_cast<size_t>(dims[1] * s[1]));
+  p.srcPos = make_hipPos(0, 0, 0);
+  p.dstPos = make_hipPos(static_cast<size_t>(c[2] * s[2]) * eb, static_cast<size_t>(c[1] * s[1]),
+                         static_cast<size_t>(c[0] * s[0]));
+  p.extent = make_hipExtent(row, static_cast<size_t>(s[1]), static_cast<size_t>(s[0]));
+  p.kind = hipMemcpyDeviceToDevice;
+  IGG_HIP_CHECK(hipMemcpy3DAsync(&p, stream));
+}
+
+}  // namespace
+
 PullGatherer::PullGatherer(int rank, int nranks, AllGather allgather)
-    : rank_(rank), nranks_(nranks), allgather_(std::move(allgather)) {}
+    : rank_(rank), nranks_(nranks), allgather_(std::move(allgather)) {
+  peer_key_.assign(nranks, std::string());
+  peer_ev_.assign(nranks, nullptr);
+}
 
 PullGatherer::~PullGatherer() {
-  if (side_) (void)hipStreamSynchronize(side_);
+  for (hipStream_t s : side_) (void)hipStreamSynchronize(s);
   for (auto& o : opened_) (void)hipIpcCloseMemHandle(o.second);
   opened_.clear();
-  if (buf_) (void)hipFree(buf_);
-  if (done_) (void)hipEventDestroy(done_);
-  if (side_) (void)hipStreamDestroy(side_);
+  for (hipEvent_t& e : peer_ev_)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : done_) (void)hipEventDestroy(e);
+  if (ready_) (void)hipEventDestroy(ready_);
+  for (hipStream_t s : side_) (void)hipStreamDestroy(s);
+}
+
+void PullGatherer::ensure_streams() {
+  if (!ready_)
+    IGG_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventInterprocess | hipEventDisableTiming));
+  while (static_cast<int>(side_.size()) < std::min(nranks_, MAX_COPY_STREAMS)) {
+    hipStream_t s;
+    hipEvent_t e;
+    IGG_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    IGG_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    side_.push_back(s);
+    done_.push_back(e);
+  }
 }
 
 void PullGatherer::free() {
   if (pending_) fail("gather_async: free while a gather is pending (call wait() first)");
-  if (side_) IGG_HIP_CHECK(hipStreamSynchronize(side_));
+  for (hipStream_t s : side_) IGG_HIP_CHECK(hipStreamSynchronize(s));
   for (auto& o : opened_) (void)hipIpcCloseMemHandle(o.second);
   opened_.clear();
-  if (buf_) {
-    IGG_HIP_CHECK(hipDeviceSynchronize());
-    IGG_HIP_CHECK(hipFree(buf_));
-  }
-  buf_ = nullptr;
-  bytes_ = 0;
 }
 
-void PullGatherer::start(const Field& a, int root, const Int3& dims) {
+void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream) {
   TraceRange tr("igg.gather_async.start");
   if (pending_) fail("gather_async: a gather is already pending (call wait() first)");
   if (!a.device) fail("gather_async: the local array must be a GPU array.");
   if (dims[0] * dims[1] * dims[2] != nranks_) fail("gather_async: dims do not match the number of processes.");
-  const size_t blk = static_cast<size_t>(a.size[0] * a.size[1] * a.size[2]) * a.elem_bytes;
-  if (!side_) {
-    IGG_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-    IGG_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
-  }
-  // `a` must be final before the root's copy engines read it.
-  IGG_HIP_CHECK(hipDeviceSynchronize());
-  std::string mine;
+  if (rank_ == root && !dst) fail("The input argument A_global can't be `nothing` on the root");
+  ensure_streams();
+  // `a` is final where the caller's stream has got to now: an interprocess
+  // event marks that point (the root's copies wait on it; no host drain).
+  IGG_HIP_CHECK(hipEventRecord(ready_, stream));
+  hipIpcEventHandle_t eh;
+  IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, ready_));
+  std::string mine(reinterpret_cast<const char*>(&eh), sizeof(eh));
   if (rank_ != root) {
     void* base = nullptr;
     size_t size = 0;
@@ -96,52 +131,59 @@ void PullGatherer::start(const Field& a, int root, const Int3& dims) {
     hipIpcMemHandle_t h;
     IGG_HIP_CHECK(hipIpcGetMemHandle(&h, base));
     const uint64_t off = a.ptr - reinterpret_cast<uintptr_t>(base);
-    mine.assign(reinterpret_cast<const char*>(&h), sizeof(h));
+    mine.append(reinterpret_cast<const char*>(&h), sizeof(h));
     mine.append(reinterpret_cast<const char*>(&off), sizeof(off));
   }
+  // Host rendezvous only (every rank has recorded its event before the root
+  // waits on it), not a GPU drain.
   const std::vector<std::string> all = allgather_(mine);
+  used_ = 0;
   if (rank_ == root) {
-    const size_t need = blk * static_cast<size_t>(nranks_);
-    if (bytes_ < need) {
-      if (buf_) {
-        IGG_HIP_CHECK(hipDeviceSynchronize());
-        IGG_HIP_CHECK(hipFree(buf_));
-      }
-      IGG_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&buf_), need));
-      bytes_ = need;
-    }
+    const size_t EH = sizeof(hipIpcEventHandle_t), MH = sizeof(hipIpcMemHandle_t);
+    const int nside = static_cast<int>(side_.size());
     for (int p = 0; p < nranks_; ++p) {
-      char* dst = buf_ + static_cast<size_t>(p) * blk;
+      const Int3 c{p / (dims[1] * dims[2]), (p / dims[2]) % dims[1], p % dims[2]};
+      hipStream_t s = side_[p % nside];
+      const void* src = nullptr;
       if (p == root) {
-        IGG_HIP_CHECK(hipMemcpyAsync(dst, reinterpret_cast<const void*>(a.ptr), blk, hipMemcpyDeviceToDevice, side_));
-        continue;
+        IGG_HIP_CHECK(hipStreamWaitEvent(s, ready_, 0));
+        src = reinterpret_cast<const void*>(a.ptr);
+      } else {
+        const std::string& rec = all[p];
+        if (rec.size() != EH + MH + 8) fail("gather_async: malformed handles from rank ", p);
+        const std::string ekey = rec.substr(0, EH);
+        if (peer_key_[p] != ekey) {  // opened once per peer event
+          if (peer_ev_[p]) IGG_HIP_CHECK(hipEventDestroy(peer_ev_[p]));
+          hipIpcEventHandle_t peh;
+          std::memcpy(&peh, ekey.data(), EH);
+          IGG_HIP_CHECK(hipIpcOpenEventHandle(&peer_ev_[p], peh));
+          peer_key_[p] = ekey;
+        }
+        IGG_HIP_CHECK(hipStreamWaitEvent(s, peer_ev_[p], 0));
+        uint64_t off = 0;
+        std::memcpy(&off, rec.data() + EH + MH, 8);
+        // Mapped for this gather only: the peer may free its array after wait().
+        void* base = ipc_open(rec.substr(EH, MH));
+        opened_.emplace_back(rec.substr(EH, MH), base);
+        src = static_cast<const char*>(base) + off;
       }
-      const std::string& rec = all[p];
-      if (rec.size() != sizeof(hipIpcMemHandle_t) + 8) fail("gather_async: malformed handle from rank ", p);
-      const std::string hkey = rec.substr(0, sizeof(hipIpcMemHandle_t));
-      uint64_t off = 0;
-      std::memcpy(&off, rec.data() + sizeof(hipIpcMemHandle_t), 8);
-      // Mapped for this gather only: the peer may free its array after wait().
-      void* base = ipc_open(hkey);
-      opened_.emplace_back(hkey, base);
-      IGG_HIP_CHECK(hipMemcpyAsync(dst, static_cast<const char*>(base) + off, blk, hipMemcpyDeviceToDevice, side_));
+      copy_block(src, dst, a.size, dims, c, a.elem_bytes, s);
     }
-    IGG_HIP_CHECK(hipEventRecord(done_, side_));
+    used_ = std::min(nranks_, nside);
+    for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipEventRecord(done_[k], side_[k]));
   }
-  field_ = a;
   root_ = root;
-  dims_ = dims;
   pending_ = true;
 }
 
-void PullGatherer::wait(void* dst, hipStream_t stream) {
+void PullGatherer::wait(hipStream_t stream) {
   TraceRange tr("igg.gather_async.wait");
   if (!pending_) fail("gather_async: no pending gather");
   if (rank_ == root_) {
-    if (!dst) fail("The input argument A_global can't be `nothing` on the root");
-    IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_, 0));
-    launch_gather_reorder(buf_, dst, field_.size, dims_, field_.elem_bytes, stream);
-    IGG_HIP_CHECK(hipEventSynchronize(done_));  // pulls done: peers may reuse their arrays
+    for (int k = 0; k < used_; ++k) {
+      IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_[k], 0));  // later work on A_global
+      IGG_HIP_CHECK(hipEventSynchronize(done_[k]));             // pulls done: peers may reuse their arrays
+    }
     for (auto& o : opened_) ipc_close(o.second);
     opened_.clear();
   }

@@ -42,16 +42,22 @@ class Gatherer {
   size_t bytes_ = 0;
 };
 
-// Non-blocking gather by root pull (MI355X copy engines). start(): every rank
-// drains its stream (so `a` is final), publishes the IPC handle + offset of the
-// allocation holding `a`; the root enqueues one hipMemcpyAsync per peer
-// (peer -> root staging buffer: a P2P copy over xGMI executed by the SDMA
-// engines, no compute units) plus its own block on a private stream, and
-// returns immediately: the application keeps computing while the data moves.
-// wait(): the root orders the caller's stream after the pulls and reorders
-// into the global layout; every rank then passes a barrier, after which the
-// peers may modify `a` again (MPI_Igather semantics: `a` is read-only until
-// wait() returns). Peer mappings live from start() to wait() only.
+// Non-blocking gather by root pull (MI355X copy engines), stream-ordered.
+// start(): every rank records an interprocess event on its own stream where
+// `a` is final (no host-side drain of the GPU) and publishes that event's IPC
+// handle plus the IPC handle + offset of the allocation holding `a`; the root
+// makes its copy streams wait on every rank's event and enqueues, per block,
+// ONE 3-D copy from the (peer-mapped) block straight into its place in
+// `dst` (hipMemcpy3DAsync: rows of s2 elements at the global pitch; a P2P copy
+// over xGMI for peer blocks). No staging buffer and no reorder pass: the
+// global array is written once. Blocks are spread over up to 8 copy streams so
+// the transfers from different peers (different xGMI links) run concurrently.
+// start() returns immediately: the application keeps computing while the
+// data moves. wait(): the root orders the caller's stream after the copies and
+// waits for them; every rank then passes a barrier, after which the peers may
+// modify `a` again (MPI_Igather semantics: `a` is read-only until wait()
+// returns). Peer memory mappings live from start() to wait(); peer events are
+// opened once and cached.
 class PullGatherer {
  public:
   using AllGather = std::function<std::vector<std::string>(const std::string&)>;
@@ -59,22 +65,25 @@ class PullGatherer {
   ~PullGatherer();
   PullGatherer(const PullGatherer&) = delete;
   PullGatherer& operator=(const PullGatherer&) = delete;
-  void start(const Field& a, int root, const Int3& dims);
-  void wait(void* dst, hipStream_t stream);
+  // `dst` (root only): C-contiguous device array of extent dims*size; `stream`:
+  // the stream on which `a` is produced (and, on the root, dst is consumed).
+  void start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream);
+  void wait(hipStream_t stream);
   bool pending() const { return pending_; }
   void free();
 
  private:
+  void ensure_streams();
   int rank_, nranks_;
   AllGather allgather_;
-  hipStream_t side_ = nullptr;
-  hipEvent_t done_ = nullptr;
-  char* buf_ = nullptr;
-  size_t bytes_ = 0;
+  std::vector<hipStream_t> side_;  // copy streams (root)
+  std::vector<hipEvent_t> done_;   // one per copy stream
+  hipEvent_t ready_ = nullptr;     // interprocess: `a` final on the caller's stream
+  std::vector<std::string> peer_key_;  // IPC event handle bytes per rank (cache key)
+  std::vector<hipEvent_t> peer_ev_;    // opened peer events (root)
   bool pending_ = false;
   int root_ = 0;
-  Field field_{};
-  Int3 dims_{1, 1, 1};
+  int used_ = 0;  // copy streams used by the pending gather
   std::vector<std::pair<std::string, void*>> opened_;  // peer mappings of the pending gather
 };
 

@@ -129,8 +129,7 @@ class GatherHandle:
     def wait(self) -> None:
         if self._done:
             return
-        dst = self._A_global
-        _puller.wait(dst.data_ptr() if dst is not None else 0, torch.cuda.current_stream().cuda_stream)
+        _puller.wait(torch.cuda.current_stream().cuda_stream)
         self._done = True
 
     @property
@@ -141,10 +140,13 @@ class GatherHandle:
 def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) -> GatherHandle:
     """Non-blocking ``gather_``: returns a handle whose ``wait()`` (collective)
     completes it. GPU fields on several ranks: the root pulls every block with
-    the copy engines (peer-to-peer hipMemcpyAsync over xGMI, no compute units)
-    while the application continues; ``A`` must not be modified before
-    ``wait()`` (MPI_Igather semantics) and ``A_global`` (root) must be a
-    C-contiguous GPU tensor. Other cases complete synchronously."""
+    the copy engines straight into its place in ``A_global`` (one 3-D
+    peer-to-peer copy per block over xGMI, ordered after the point of every
+    rank's current stream where ``A`` is final by interprocess events: no GPU
+    drain at the call, no compute units, no staging buffer) while the
+    application continues; ``A`` must not be modified before ``wait()``
+    (MPI_Igather semantics) and ``A_global`` (root) must be a C-contiguous GPU
+    tensor. Other cases complete synchronously."""
     global _puller
     gg = _grid.global_grid()
     nprocs, me = int(gg.nprocs), int(gg.me)
@@ -167,7 +169,8 @@ def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int =
         c = gg.comm
         _puller = native.PullGatherer(me, nprocs, lambda b: c.all_gather_object(bytes(b)))
     dims = [int(d) for d in gg.dims]
-    _puller.start(field_tuple(A), root, dims)
+    _puller.start(field_tuple(A), A_global.data_ptr() if me == root else 0, root, dims,
+                  torch.cuda.current_stream().cuda_stream)
     return GatherHandle(A_global if me == root else None, False)
 
 

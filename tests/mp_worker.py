@@ -215,15 +215,24 @@ def scenario_gather_async():
     s = (6, 5, 4)
     for root in sorted({0, nprocs - 1}):
         for dt in (torch.float64, torch.float32):
-            A = (torch.full(s, float(me + 1), dtype=torch.float64) * 1000
-                 + torch.arange(120, dtype=torch.float64).view(s)).to(dt).cuda()
+            final = (torch.full(s, float(me + 1), dtype=torch.float64) * 1000
+                     + torch.arange(120, dtype=torch.float64).view(s)).to(dt).cuda()
+            A = torch.zeros(s, dtype=dt, device="cuda")
             G = torch.zeros(dims[0] * 6, dims[1] * 5, dims[2] * 4, dtype=dt, device="cuda") if me == root else None
+            torch.cuda.synchronize()
+            # A becomes final only behind a long kernel on this rank's stream and
+            # gather_async_ is called without a host sync: the root's pull must
+            # be ordered after that point (interprocess events), not before.
+            delay = torch.rand(1536, 1536, device="cuda", dtype=torch.float64)
+            for _ in range(4):
+                delay = delay @ delay * 1e-3
+            A.copy_(final)
             h = igg.gather_async_(A, G, root=root)
             busy = torch.rand(256, 256, device="cuda") @ torch.rand(256, 256, device="cuda")  # overlapped work
             h.wait()
             A.fill_(-1)  # allowed after wait()
             torch.cuda.synchronize()
-            del busy
+            del busy, delay
             if me == root:
                 Gc = G.cpu().double()
                 for p in range(nprocs):

@@ -119,15 +119,24 @@ def test_gpu_gather_single(gpu):
     igg.finalize_global_grid(finalize_MPI=False)
 
 
-def test_gpu_gather_reorder_kernel(gpu):
-    """The root-side block reorder kernel vs a torch permute."""
+@pytest.mark.parametrize("s,dims,dtype", [
+    ((3, 4, 5), (2, 3, 2), torch.float32),      # 20-byte rows: element path
+    ((3, 4, 8), (2, 3, 2), torch.float32),      # 32-byte rows: 16-byte units
+    ((5, 3, 7), (1, 2, 3), torch.float16),      # 2-byte elements, odd rows
+    ((4, 6, 130), (2, 2, 2), torch.float64),    # rows longer than one wave pass
+    ((2, 3, 300), (2, 1, 3), torch.complex128),  # 16-byte elements
+    ((7, 1, 1), (3, 1, 1), torch.int16),        # 1-element rows
+])
+def test_gpu_gather_reorder_kernel(gpu, s, dims, dtype):
+    """The root-side block reorder kernel (one wave per row) vs a torch permute."""
     from igg._native import native
 
-    s, dims = (3, 4, 5), (2, 3, 2)
     nb = dims[0] * dims[1] * dims[2]
-    src = torch.arange(nb * 60, dtype=torch.float32, device=gpu)
-    dst = torch.empty(nb * 60, dtype=torch.float32, device=gpu)
-    native.gather_reorder(src.data_ptr(), dst.data_ptr(), list(s), list(dims), 4, torch.cuda.current_stream().cuda_stream)
+    n = s[0] * s[1] * s[2]
+    src = torch.arange(nb * n, dtype=torch.float64, device=gpu).to(dtype)
+    dst = torch.full((nb * n,), -1, dtype=torch.float64, device=gpu).to(dtype)
+    native.gather_reorder(src.data_ptr(), dst.data_ptr(), list(s), list(dims), src.element_size(),
+                          torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     ref = src.view(*dims, *s).permute(0, 3, 1, 4, 2, 5).reshape(-1)
     assert torch.equal(dst, ref)
