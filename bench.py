@@ -203,12 +203,40 @@ def _sync(comm=None) -> None:
     bounded_device_sync(what="bench", comm=comm)
 
 
+# Barrier flavour of the timed regions (set in main once RCCL is validated).
+_BRACKET = {"dev": False, "gpu": True}
+
+
+def _bracket(comm) -> None:
+    """One side of a timed region: a barrier of all ranks + synchronize.
+    GPU, several ranks with a validated RCCL communicator: a one-element RCCL
+    all-reduce on the stream (it completes on a rank only once every rank has
+    reached it: tens of us over xGMI), a bounded event poll of the stream
+    (microseconds after completion; aborts RCCL on a dead peer) and
+    torch.cuda.synchronize(). Otherwise drain, then the host barrier (gloo:
+    0.2-0.7 ms, i.e. 2-5 % of a 20-step region: profiles/r2_bracket/)."""
+    import torch
+
+    if not _BRACKET["gpu"]:
+        comm.barrier()
+        return
+    from igg.parallel.comm import bounded_stream_sync
+
+    if _BRACKET["dev"] and comm.size > 1:
+        comm.device_barrier()
+        bounded_stream_sync(what="bench", comm=comm)
+    else:
+        bounded_stream_sync(what="bench", comm=comm)
+        comm.barrier()
+    torch.cuda.synchronize()
+
+
 def _timed(model, comm, k: int) -> float:
     _sync(comm)
-    comm.barrier()
+    _bracket(comm)
     t0 = time.perf_counter()
     model.run(k)
-    _sync(comm)
+    _bracket(comm)
     return _max_over_ranks(comm, time.perf_counter() - t0) / k
 
 
@@ -459,6 +487,7 @@ def main():
         A_global = torch.empty([int(d) * int(s) for d, s in zip(dims, field().shape)],
                                dtype=dtype, device=field().device)
     graph_ok = args.graph and on_gpu
+    _BRACKET["gpu"], _BRACKET["dev"] = on_gpu, False
     valid, ab = None, None
     if on_gpu and nprocs > 1:
         ref = "staged"
@@ -466,6 +495,7 @@ def main():
         if args.share_gpu:  # ranks share one device: RCCL refuses duplicate GPUs
             names = ["put"]
         valid = validate_transports(field(), comm, log, ref=ref, names=names)
+        _BRACKET["dev"] = bool(comm.rccl is not None and valid.get("rccl-sequential") == "ok")
         if args.share_gpu and valid.get("put") != "ok":
             H.set_transport("staged")
         elif not args.overlap:
@@ -504,8 +534,7 @@ def main():
         extra = int(-(-warm_ms // (est * k))) * k
         model.run(extra)
     sync()
-    comm.barrier()
-    sync()
+    _bracket(comm)
     t0 = time.perf_counter()
     if gather_every > 0:
         done, pending = 0, None
@@ -528,8 +557,7 @@ def main():
             pending.wait()
     else:
         model.run(args.steps)
-    sync()
-    comm.barrier()
+    _bracket(comm)
     t1 = time.perf_counter()
     elapsed = _max_over_ranks(comm, t1 - t0)
     H.check_transport()
@@ -614,6 +642,8 @@ def main():
                 "self_launched": os.environ.get("IGG_BENCH_SELF_LAUNCHED") == "1",
                 "hip_graph": getattr(model, "graph", None) is not None,
                 "hip_graph_error": graph_error,
+                "timing_bracket": ("rccl all-reduce + stream event + synchronize" if _BRACKET["dev"] and nprocs > 1
+                                   else ("host barrier + stream event + synchronize" if on_gpu else "host barrier")),
             },
         }
         print(json.dumps(out), flush=True)

@@ -7,6 +7,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
+#include <thread>
+
 #include <hip/hip_runtime_api.h>
 
 #include "igg/acoustic.hpp"
@@ -150,6 +153,25 @@ PYBIND11_MODULE(_igg_native, m) {
     py::gil_scoped_release nogil;
     IGG_HIP_CHECK(hipDeviceSynchronize());
   });
+  // Bounded, low-latency wait for everything enqueued on stream `s` so far:
+  // an event recorded there is polled (GIL released) until it completes or
+  // `timeout` seconds pass (returns false; the caller aborts communicators).
+  // Unlike a helper thread around hipDeviceSynchronize it returns within
+  // microseconds of completion, so a timed region pays no wake-up latency.
+  m.def("stream_wait_bounded", [](uintptr_t s, double timeout) {
+    thread_local hipEvent_t ev = nullptr;
+    if (!ev) IGG_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    IGG_HIP_CHECK(hipEventRecord(ev, as_stream(s)));
+    py::gil_scoped_release nogil;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipEventQuery(ev);
+      if (e == hipSuccess) return true;
+      if (e != hipErrorNotReady) IGG_HIP_CHECK(e);
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout) return false;
+      std::this_thread::yield();
+    }
+  }, py::arg("stream"), py::arg("timeout"));
   m.def("stream_synchronize", [](uintptr_t s) {
     py::gil_scoped_release nogil;
     IGG_HIP_CHECK(hipStreamSynchronize(as_stream(s)));

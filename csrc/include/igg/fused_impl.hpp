@@ -1,0 +1,539 @@
+#pragma once
+// Fused halo-exchange diffusion kernel templates for gfx950 (included by the
+// csrc/kernels/fused_*.hip translation units; see igg/fused.hpp).
+//
+// Same 2.5-D blocked, vectorised sweep as diffusion3d_vkernel (stencil_kernels.hip)
+// over the inner box [1, n-1)^3, plus the exchange of the update_halo! step
+// (reference: src/update_halo.jl:32-78 after examples/diffusion3D_*:42-46):
+//   * receive: the face halos are read from this rank's arena regions (written
+//     by the neighbours' previous step) instead of the field's halo planes -
+//     dim 0 by redirecting the plane base of x=0 / n0-1, dim 1 by redirecting
+//     the base of the y=0 / n1-1 rows, dim 2 element-wise (below);
+//   * send: the values of the planes x=1/n0-2, rows y=1/n1-2 and elements
+//     z=1/n2-2 are stored into the receivers' arenas (IPC-mapped
+//     peer memory: the stores travel over xGMI while the sweep goes on).
+// Every pointer is a separate __restrict__ kernel argument so the compiler
+// knows the remote stores never alias the T/Cp loads and keeps the plain
+// kernel's load schedule. The z edge (one element per row, in lane 0 of the
+// first segment and lane zh of the last) moves lane-distributed: the halo
+// values of the RY rows are fetched one x step ahead by lanes r / 32+r with
+// ONE load instruction and patched into the edge lane with readlane; the
+// send values are gathered the same way and leave with ONE store per step.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "igg/stencil.hpp"
+
+
+namespace igg {
+
+// Diagnostics state set by fused_debug() and copied into the next launches
+// (defined in fused_kernels.hip).
+extern int64_t* g_hx_stamps;
+extern int g_hx_force_sel;
+
+// Fused launches by tiling family, one translation unit each (compiled in
+// parallel): fused_t0.hip (variants 0, 50), fused_t11.hip (11, 40, 41),
+// fused_misc.hip (2, 9, 14). Return false for a variant not in the family.
+bool fused_launch_t0(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
+bool fused_launch_t11(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
+bool fused_launch_misc(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
+
+namespace {
+
+template <typename T, int VZ>
+struct Vec {
+  typedef T type __attribute__((ext_vector_type(VZ)));
+};
+
+template <typename T, int VZ>
+__device__ __forceinline__ typename Vec<T, VZ>::type vld(const T* p) {
+  return *reinterpret_cast<const typename Vec<T, VZ>::type*>(p);
+}
+
+template <typename T>
+__device__ __forceinline__ T lane_read(T v, int l) {
+  if constexpr (sizeof(T) == 8) {
+    const int2 p = __builtin_bit_cast(int2, v);
+    return __builtin_bit_cast(T, make_int2(__builtin_amdgcn_readlane(p.x, l), __builtin_amdgcn_readlane(p.y, l)));
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  }
+}
+
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+// Block chunk index in march order (chunks holding the x send planes first).
+__device__ __forceinline__ int64_t hx_chunk(int64_t cxr, int64_t nch) {
+  return (cxr == 0 || nch < 2) ? cxr : (cxr == 1 ? nch - 1 : cxr - 1);
+}
+
+template <typename T>
+struct HxScal {
+  int64_t n0, n1, n2, zp;
+  int64_t ntz, nty, ch;  // z tiles, y tiles, planes per chunk
+  T rdx2, rdy2, rdz2, dtlam;
+  // Diagnostics (fused_debug): per-wave {class, start, end, cu} stamps
+  // (wall_clock64 ticks) into `stamps` (4 int64 per wave) when non-null;
+  // force_sel >= 0 runs every wave with that feature class.
+  int64_t* stamps;
+  int force_sel;
+};
+
+
+// FEAT bits (compile-time exchange features): 1 x-in, 2 y-in, 4 z-in, 8 z-out,
+// 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants); 512 =
+// lane-distributed z-segment edge loads (plain variants, below); 1024 = one
+// workgroup per CU (launch); 2048 = no per-wave specialisation (kernel below);
+// 4096 = z edge values staged through LDS instead of v_readlane. 207 = the full
+// exchange, 0 = the plain update (variants 21+); other subsets served the cost
+// bisect (profiles/r1_fused/feature_bisect_*).
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT>
+__device__ __forceinline__ void
+hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
+         const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
+         const T* __restrict__ yi1, const T* __restrict__ zi0, const T* __restrict__ zi1,
+         T* __restrict__ xo0, T* __restrict__ xo1, T* __restrict__ yo0, T* __restrict__ yo1,
+         T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T>& a) {
+  using V = typename Vec<T, VZ>::type;
+  constexpr int W = 64 * VZ * BZ;
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t tz = b % a.ntz;
+  const int64_t rest = b / a.ntz;
+  const int64_t ty = rest % a.nty;
+  // Chunks holding the x send planes run first (order 0, last, 1, 2, ...): the
+  // plane x=n0-2 is computed in the last step of the last chunk, so with >= 2
+  // residency rounds its remote stores drain while later rounds compute
+  // instead of at the kernel's tail. Scheduling only: results are unchanged.
+  const int64_t nch = (a.n0 - 2 + a.ch - 1) / a.ch;
+  const int64_t cxr = rest / a.nty;
+  const int64_t cx = hx_chunk(cxr, nch);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wz = wid % BZ, wy = wid / BZ;
+  const int64_t n0 = a.n0, n1 = a.n1, n2 = a.n2, s0 = n1 * n2;
+  const int64_t zt = tz * W + wz * (64 * VZ);
+  const int64_t y0 = 1 + ty * (BY * RY) + wy * RY;
+  const int64_t xs = 1 + cx * a.ch;
+  const int64_t xe = min(xs + a.ch, n0 - 1);
+  const int nv = static_cast<int>(min<int64_t>(RY, n1 - 1 - y0));
+  if (nv <= 0 || xs >= xe) return;
+  const int64_t hi2 = n2 - 1;
+  if (zt >= hi2) return;
+  const int64_t z0 = zt + lane * VZ;
+  const int64_t zhi_v = ((hi2 - 1) / VZ) * VZ;
+  const int64_t zc = min(z0, zhi_v);
+  const int zl = static_cast<int>(zc - zt);
+  const bool lane_full = z0 >= 1 && z0 + VZ <= hi2;
+  // Lanes past the box alias the last valid vector (zc < z0) and compute
+  // garbage there: they must not store (remote whole-vector stores included).
+  const bool zown = zc == z0;
+  const bool load_prev = lane == 0;
+  const bool load_next = lane == 63 || z0 + VZ > zhi_v;
+  const int zpi = static_cast<int>(max<int64_t>(zc - 1, 0) - zt);
+  const int zni = static_cast<int>(min<int64_t>(zc + VZ, n2 - 1) - zt);
+  // FEAT 512: the z neighbours across the segment's ends (lane 0's prev, the
+  // load_next lanes' next: one uniform element per row each) are fetched by
+  // lanes r / 32+r with ONE load per x step, one step ahead, and moved with
+  // readlane - instead of 2*RY single-lane loads held in 2*RY registers.
+  static_assert(!(FEAT & 512) || RY <= 32, "FEAT 512: at most 32 rows per wave");
+  const int64_t zc63 = min<int64_t>(zt + 63 * VZ, zhi_v);
+  const int zedge = lane < 32 ? static_cast<int>(max<int64_t>(zt - 1, 0) - zt)
+                              : static_cast<int>(min<int64_t>(zc63 + VZ, n2 - 1) - zt);
+  const int64_t rowe = (y0 + min(lane & 31, nv - 1)) * n2 + zt + zedge;
+
+  int64_t rowb[RY];
+#pragma unroll
+  for (int r = 0; r < RY; ++r) rowb[r] = (y0 + min(r, nv - 1)) * n2 + zt;
+  // y-neighbour rows outside the wave (dim-1 halo rows come from the arena).
+  const T* ymb = t + (y0 - 1) * n2 + zt;
+  const T* ypb = t + (y0 + nv) * n2 + zt;
+  int64_t yms = s0, yps = s0;
+  if ((FEAT & 2) && y0 == 1 && yi0) { ymb = yi0 + zt; yms = n2; }
+  if ((FEAT & 2) && y0 + nv == n1 - 1 && yi1) { ypb = yi1 + zt; yps = n2; }
+  // y send rows of this wave.
+  T* const yrow0 = ((FEAT & 128) && y0 == 1 && yo0) ? yo0 + zt : nullptr;
+  int ry1 = static_cast<int>(n1 - 2 - y0);
+  T* const yrow1 = ((FEAT & 128) && ry1 >= 0 && ry1 < nv && yo1) ? yo1 + zt : nullptr;
+  if (!yrow1) ry1 = -1;
+  // z edges of this wave: low edge in lane 0 (element 0 = halo z=0, element
+  // 1 = send z=1), high edge in lane zh (element VZ-1 = halo, VZ-2 = send).
+  const bool has_lo = zt == 0, has_hi = zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ;
+  // readfirstlane: the compiler must see zh as uniform, or every readlane
+  // with it becomes a waterfall loop draining vmcnt (measured +27 % per step).
+  const int zh = __builtin_amdgcn_readfirstlane(static_cast<int>((n2 - VZ - zt) / VZ));
+  const bool zin_lo = (FEAT & 4) && has_lo && zi0, zin_hi = (FEAT & 4) && has_hi && zi1;
+  const bool zout_lo = (FEAT & 8) && has_lo && zo0, zout_hi = (FEAT & 8) && has_hi && zo1;
+  const bool zin = zin_lo || zin_hi, zout = zout_lo || zout_hi;
+  const int rl = lane & 31;
+  // Lane-distributed z values: row r of the low edge in lane r, of the high
+  // edge in lane 32+r (rows < nv).
+  const bool lo_l = lane < 32 && rl < nv, hi_l = lane >= 32 && rl < nv;
+  // Every lane loads (lanes without a row of their own read a valid dummy in
+  // the same region): a load under a per-lane condition would be a divergent
+  // branch around a load in the hot loop, which costs the loop its prefetch.
+  const T* zsrc = lo_l && zin_lo ? zi0 + (y0 - 1) + rl
+                                 : (hi_l && zin_hi ? zi1 + (y0 - 1) + rl
+                                                   : (zin_lo ? zi0 : zi1) + (y0 - 1));
+  T* zdst = lo_l && zout_lo ? zo0 + (y0 - 1) + rl : (hi_l && zout_hi ? zo1 + (y0 - 1) + rl : nullptr);
+  const bool remote = zout || yrow0 || yrow1 || (xs == 1 && xo0) || (xe == n0 - 1 && xo1);
+  T znext = T(0), zv = T(0);
+  if (zin) znext = zsrc[xs * a.zp];
+  // FEAT 4096: the z edge values move between the edge lane and the
+  // lane-distributed row layout through 4*RY LDS slots of this wave (in/out x
+  // lo/hi) instead of v_readlane (whose SGPR result feeds VALU with wait states
+  // that one wave per SIMD cannot hide: profiles/r2_fused_spec/).
+  T* zs = nullptr;
+  if constexpr ((FEAT & 4096) != 0) {
+    __shared__ T zslots[BY * BZ * 4 * RY];
+    zs = zslots + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (4 * RY);
+  }
+  // Deferred sends (DF): the y row / z values of step x leave after the loads
+  // of step x+1 were issued, so their acknowledgement never gates those loads.
+  V ysend;
+  T* ysend_dst = nullptr;
+  T* zsend_dst = nullptr;
+
+  auto plane = [&](int64_t X) -> const T* {
+    if constexpr ((FEAT & 1) != 0) {
+      if (X == 0 && xi0) return xi0;
+      if (X == n0 - 1 && xi1) return xi1;
+    }
+    return t + X * s0;
+  };
+  // Cp is streamed once (no reuse): FEAT bit 256 loads it non-temporally so it
+  // does not displace the T lines that neighbouring waves re-read (y/z halos).
+  auto ldc = [&](const T* p) -> V {
+    if constexpr ((FEAT & 256) != 0) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+    return vld<T, VZ>(p);
+  };
+  V tm[RY], tc[RY], tp[RY], cp[RY];
+#pragma unroll
+  for (int r = 0; r < RY; ++r) {
+    tm[r] = vld<T, VZ>(plane(xs - 1) + rowb[r] + zl);
+    tc[r] = vld<T, VZ>(plane(xs) + rowb[r] + zl);
+    tp[r] = vld<T, VZ>(plane(xs + 1) + rowb[r] + zl);
+    cp[r] = ldc(cpp + xs * s0 + rowb[r] + zl);
+  }
+  const T two = T(2);
+  T evn = T(0);
+  if constexpr ((FEAT & 512) != 0) evn = t[xs * s0 + rowe];
+  for (int64_t x = xs; x < xe; ++x) {
+    const int64_t off = x * s0;
+    T evc = T(0);
+    if constexpr ((FEAT & 512) != 0) {
+      evc = evn;
+      if (x + 1 < xe) evn = t[off + s0 + rowe];
+    }
+    // z halo of plane x (fetched one step ahead), prefetch plane x+1's. (The
+    // alternative of substituting it at its use measured slower for every
+    // tiling: profiles/r1_fused/feature_bisect_v11_zin_alt.log.)
+    if (zin) {
+      const T zcur = znext;
+      if (x + 1 < xe) znext = zsrc[(x + 1) * a.zp];
+      if constexpr ((FEAT & 4096) != 0) {
+        // through the wave's LDS slots: no v_readlane -> SGPR -> VALU chain
+        if (lo_l || hi_l) zs[(lane < 32 ? 0 : RY) + rl] = zcur;
+#pragma unroll
+        for (int r = 0; r < RY; ++r) {
+          if (zin_lo) {
+            const T v = zs[r];
+            if (lane == 0) tc[r][0] = v;
+          }
+          if (zin_hi) {
+            const T v = zs[RY + r];
+            if (lane == zh) tc[r][VZ - 1] = v;
+          }
+        }
+      } else {
+        // Branch-free: per-row uniform branches split the loop body into
+        // basic blocks the scheduler cannot interleave across, which at one
+        // wave per SIMD serialises the rows (profiles/r2_fused_spec/).
+        const bool pl = zin_lo && lane == 0, ph = zin_hi && lane == zh;
+#pragma unroll
+        for (int r = 0; r < RY; ++r) {
+          const T vl = lane_read(zcur, r), vh = lane_read(zcur, 32 + r);
+          tc[r][0] = pl ? vl : tc[r][0];
+          tc[r][VZ - 1] = ph ? vh : tc[r][VZ - 1];
+        }
+      }
+    }
+    T* const xd0 = (FEAT & 64) && x == 1 ? xo0 : nullptr;
+    T* const xd1 = (FEAT & 64) && x == n0 - 2 ? xo1 : nullptr;
+    V tn[RY], cpn[RY];
+    if (PF) {
+      const int64_t xn = min(x + 2, n0 - 1), xc = min(x + 1, xe - 1);
+      const T* pn = ((FEAT & 1) && xn == n0 - 1 && xi1) ? xi1 : t + xn * s0;
+#pragma unroll
+      for (int r = 0; r < RY; ++r) {
+        tn[r] = vld<T, VZ>(pn + rowb[r] + zl);
+        cpn[r] = ldc(cpp + xc * s0 + rowb[r] + zl);
+      }
+    }
+    const V ym = vld<T, VZ>(ymb + x * yms + zl);
+    const V yp = vld<T, VZ>(ypb + x * yps + zl);
+    T em[RY], ep[RY];
+    if constexpr ((FEAT & 512) == 0) {
+#pragma unroll
+      for (int r = 0; r < RY; ++r) {
+        em[r] = load_prev ? t[off + rowb[r] + zpi] : T(0);
+        ep[r] = load_next ? t[off + rowb[r] + zni] : T(0);
+      }
+    }
+    if constexpr (DF) {
+      if (ysend_dst) *reinterpret_cast<V*>(ysend_dst) = ysend;
+      if (zsend_dst) *zsend_dst = zv;
+      ysend_dst = nullptr;
+      zsend_dst = nullptr;
+    }
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      const V& c = tc[r];
+      const V& yv = (r == 0) ? ym : tc[r > 0 ? r - 1 : 0];
+      const V& yn = (r + 1 < nv) ? tc[(r + 1 < RY) ? r + 1 : r] : yp;
+      T prev = __shfl_up(c[VZ - 1], 1);
+      T next = __shfl_down(c[0], 1);
+      if constexpr ((FEAT & 512) != 0) {
+        const T pv = lane_read(evc, r), nx = lane_read(evc, 32 + r);
+        if (load_prev) prev = pv;
+        if (load_next) next = nx;
+      } else {
+        if (load_prev) prev = em[r];
+        if (load_next) next = ep[r];
+      }
+      V out;
+#pragma unroll
+      for (int e = 0; e < VZ; ++e) {
+        const T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
+        const T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
+        const T c2 = two * c[e];
+        const T lap = (tp[r][e] - c2 + tm[r][e]) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
+                      (zp - c2 + zm) * a.rdz2;
+        out[e] = c[e] + a.dtlam / cp[r][e] * lap;
+      }
+      if (r < nv) {
+        T* dst = t2 + off + rowb[r] + zl;
+        if (lane_full) {
+          __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
+        } else {
+#pragma unroll
+          for (int e = 0; e < VZ; ++e)
+            if (z0 + e >= 1 && z0 + e < hi2 && zc == z0) dst[e] = out[e];
+        }
+        // Send planes / rows (whole vectors of the lanes that own them: the
+        // halo elements they carry are never read by the receiver).
+        if (xd0 && zown) *reinterpret_cast<V*>(xd0 + rowb[r] + zl) = out;
+        if (xd1 && zown) *reinterpret_cast<V*>(xd1 + rowb[r] + zl) = out;
+        if (r == 0 && yrow0) {
+          if (DF) { ysend = out; ysend_dst = zown ? yrow0 + x * n2 + zl : nullptr; }
+          else if (zown) *reinterpret_cast<V*>(yrow0 + x * n2 + zl) = out;
+        }
+        if (r == ry1) {
+          // one deferral slot: taken by row 0 if this wave also sends that row
+          if (DF && !yrow0) { ysend = out; ysend_dst = zown ? yrow1 + x * n2 + zl : nullptr; }
+          else if (zown) *reinterpret_cast<V*>(yrow1 + x * n2 + zl) = out;
+        }
+        if constexpr ((FEAT & 4096) != 0) {
+          if (zout_lo && lane == 0) zs[2 * RY + r] = out[1];
+          if (zout_hi && lane == zh) zs[3 * RY + r] = out[VZ - 2];
+        } else if constexpr ((FEAT & 8) != 0) {
+          // branch-free (see the z-in patch): unconditional readlanes + selects
+          const T vl = lane_read(out[1], 0), vh = lane_read(out[VZ - 2], zh);
+          zv = (zout_lo && lane == r) ? vl : zv;
+          zv = (zout_hi && lane == 32 + r) ? vh : zv;
+        }
+      }
+    }
+    if constexpr ((FEAT & 4096) != 0) {
+      if (zdst) zv = zs[(lane < 32 ? 2 * RY : 3 * RY) + rl];
+    }
+    if (zdst) {
+      if (DF) zsend_dst = zdst + x * a.zp;
+      else zdst[x * a.zp] = zv;
+    }
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      tm[r] = tc[r];
+      tc[r] = tp[r];
+      if (PF) {
+        tp[r] = tn[r];
+        cp[r] = cpn[r];
+      }
+    }
+    if (!PF && x + 1 < xe) {
+      const T* pn = ((FEAT & 1) && x + 2 == n0 - 1 && xi1) ? xi1 : t + (x + 2) * s0;
+#pragma unroll
+      for (int r = 0; r < RY; ++r) {
+        tp[r] = vld<T, VZ>(pn + rowb[r] + zl);
+        cp[r] = ldc(cpp + (x + 1) * s0 + rowb[r] + zl);
+      }
+    }
+  }
+  if constexpr (DF) {  // sends of the last step
+    if (ysend_dst) *reinterpret_cast<V*>(ysend_dst) = ysend;
+    if (zsend_dst) *zsend_dst = zv;
+  }
+  // Remote stores acknowledged before the wave retires (the sync kernel that
+  // publishes the arrival flags runs after this kernel on the same stream).
+  if (remote) __builtin_amdgcn_s_waitcnt(0);
+}
+
+// The kernel: each wave runs the sweep specialised to the exchange features its
+// tile actually touches. A wave away from every exchanged face (most of them:
+// not in the first/last x chunk, not in the first/last y row of tiles, not in a
+// z-edge tile) runs the plain sweep (FEAT without exchange bits): the exchange
+// code only present in the same loop, with its pointers null at run time,
+// measured +60-70 us per step for tilings 11/40 (profiles/r2_fused_spec/),
+// because it changes the hot loop's schedule. The test is wave-uniform, so the
+// dispatch is a scalar branch; results are unchanged (the skipped features are
+// no-ops for such a wave).
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
+__global__ void __launch_bounds__(64 * BY * BZ)
+diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
+                      const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
+                      const T* __restrict__ yi1, const T* __restrict__ zi0, const T* __restrict__ zi1,
+                      T* __restrict__ xo0, T* __restrict__ xo1, T* __restrict__ yo0, T* __restrict__ yo1,
+                      T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T> a) {
+  constexpr int FX = FEAT & (1 | 64), FY = FEAT & (2 | 128), FZ = FEAT & (4 | 8);
+  constexpr int FK = FEAT & ~(1 | 2 | 4 | 8 | 64 | 128);
+#define IGG_HX_SWEEP(F)                                                                                  \
+  hx_sweep<T, BY, RY, VZ, PF, BZ, DF, (F)>(t2, t, cpp, xi0, xi1, yi0, yi1, zi0, zi1, xo0, xo1, yo0, yo1, \
+                                           zo0, zo1, a)
+  if constexpr ((FX | FY | FZ) == 0 || (FEAT & 2048) != 0) {
+    IGG_HX_SWEEP(FEAT);  // nothing to specialise, or specialisation disabled (FEAT 2048)
+  } else {
+    constexpr int W = 64 * VZ * BZ;
+    const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t rest = b / a.ntz;
+    const int64_t tz = b % a.ntz, ty = rest % a.nty;
+    const int64_t n0 = a.n0, n1 = a.n1, n2 = a.n2;
+    const int64_t nch = (n0 - 2 + a.ch - 1) / a.ch;
+    const int64_t cx = hx_chunk(rest / a.nty, nch);
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wz = wid % BZ, wy = wid / BZ;
+    const int64_t zt = tz * W + wz * (64 * VZ);
+    const int64_t y0 = 1 + ty * (BY * RY) + wy * RY;
+    const int64_t xs = 1 + cx * a.ch;
+    const int64_t xe = min(xs + a.ch, n0 - 1);
+    const int64_t nv = min<int64_t>(RY, n1 - 1 - y0);
+    // conservative: a chunk that reads plane 0 / n0-1 or computes plane 1 / n0-2
+    // Per side, and only sides with a neighbour count (a 2x1x1 rank runs no
+    // y/z code at all; a 2x2x2 corner rank only the z-edge tiles of one side).
+    const bool wx = FX != 0 && ((xs <= 1 && (xi0 || xo0)) || (xe >= n0 - 2 && (xi1 || xo1)));
+    const bool wyy = FY != 0 && ((y0 <= 1 && (yi0 || yo0)) || (y0 + nv >= n1 - 1 && (yi1 || yo1)));
+    const bool wzz = FZ != 0 && ((zt == 0 && (zi0 || zo0)) ||
+                                 (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ && (zi1 || zo1)));
+    int sel = __builtin_amdgcn_readfirstlane((wx ? 1 : 0) | (wyy ? 2 : 0) | (wzz ? 4 : 0));
+    if (a.force_sel >= 0) sel = a.force_sel;
+    const int64_t t_start = a.stamps ? wall_clock64() : 0;
+    switch (sel) {
+      case 0: IGG_HX_SWEEP(FK); break;
+      case 1: IGG_HX_SWEEP(FK | FX); break;
+      case 2: IGG_HX_SWEEP(FK | FY); break;
+      case 3: IGG_HX_SWEEP(FK | FX | FY); break;
+      case 4: IGG_HX_SWEEP(FK | FZ); break;
+      case 5: IGG_HX_SWEEP(FK | FX | FZ); break;
+      case 6: IGG_HX_SWEEP(FK | FY | FZ); break;
+      default: IGG_HX_SWEEP(FEAT); break;
+    }
+    if (a.stamps) {
+      // one vector store per wave (lane 0; lane-dependent address -> VGPR store)
+      const int lane = threadIdx.x & 63;
+      const int64_t w = (static_cast<int64_t>(blockIdx.x) * (BY * BZ) + wid) * 4;
+      if (lane < 4) {
+        int cu = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(cu));
+        const int64_t v[4] = {sel, t_start, wall_clock64(), static_cast<int64_t>(cu)};
+        a.stamps[w + lane] = v[lane];
+      }
+    }
+  }
+#undef IGG_HX_SWEEP
+}
+
+int resident(const void* kernel, int block, size_t lds = 0) {
+  static std::vector<std::pair<const void*, int>> cache;
+  for (const auto& c : cache)
+    if (c.first == kernel) return c.second;
+  int dev = 0, cus = 0, occ = 0;
+  IGG_HIP_CHECK(hipGetDevice(&dev));
+  IGG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  IGG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, lds));
+  const int r = std::max(1, occ) * std::max(1, cus);
+  cache.emplace_back(kernel, r);
+  return r;
+}
+
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
+void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream) {
+  const int64_t n0 = d.n[0], n1 = d.n[1], n2 = d.n[2];
+  if (n2 % VZ != 0 || n2 < 2 * VZ)
+    fail("diffusion3d (fused halo): n2 must be a multiple of ", VZ, " and >= ", 2 * VZ);
+  auto kern = &diffusion3d_hx_kernel<T, BY, RY, VZ, PF, BZ, DF, FEAT>;
+  const int block = 64 * BY * BZ;
+  constexpr int W = 64 * VZ * BZ, TY = BY * RY;
+  HxScal<T> a;
+  a.n0 = n0; a.n1 = n1; a.n2 = n2; a.zp = io.zpitch;
+  a.ntz = (n2 - 1 + W - 1) / W;
+  a.nty = (n1 - 2 + TY - 1) / TY;
+  const int64_t len0 = n0 - 2, tiles = a.ntz * a.nty;
+  const int rounds = d.rounds > 0 ? d.rounds : 1;
+  // FEAT 1024: one workgroup per CU, enforced with an unused dynamic LDS
+  // allocation (isolates the occupancy effect of the lower-VGPR FEAT 512 form).
+  const size_t lds = (FEAT & 1024) ? 96 * 1024 : 0;
+  const int64_t target = static_cast<int64_t>(rounds) * resident(reinterpret_cast<const void*>(kern), block, lds);
+  const int64_t ch_all = std::max<int64_t>(1, (len0 * tiles + target - 1) / target);
+  const int64_t nch = std::max<int64_t>(1, (len0 + ch_all - 1) / ch_all);
+  a.ch = (len0 + nch - 1) / nch;
+  const int64_t blocks = tiles * ((len0 + a.ch - 1) / a.ch);
+  if (blocks > 0x7fffffffLL) fail("diffusion3d (fused halo): grid too large");
+  a.rdx2 = static_cast<T>(d.rd2[0]);
+  a.rdy2 = static_cast<T>(d.rd2[1]);
+  a.rdz2 = static_cast<T>(d.rd2[2]);
+  a.dtlam = static_cast<T>(d.dt_lam);
+  a.stamps = g_hx_stamps;
+  a.force_sel = g_hx_force_sel;
+  auto in = [&](int k, int s) { return reinterpret_cast<const T*>(io.in[k][s]); };
+  auto out = [&](int k, int s) { return reinterpret_cast<T*>(io.out[k][s]); };
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(block), lds, stream,
+                     reinterpret_cast<T*>(d.t2), reinterpret_cast<const T*>(d.t), reinterpret_cast<const T*>(d.cp),
+                     in(0, 0), in(0, 1), in(1, 0), in(1, 1), in(2, 0), in(2, 1), out(0, 0), out(0, 1), out(1, 0),
+                     out(1, 1), out(2, 0), out(2, 1), a);
+  IGG_HIP_CHECK(hipGetLastError());
+}
+
+// Send ordering (FusedHalo mode): 0 = remote stores right after the values
+// are computed (fastest when stores are acknowledged quickly, e.g. loopback),
+// 1 = deferred by one x step (their acknowledgement latency over xGMI can
+// never gate the next step's loads). The z edge is lane-distributed in both
+// (a per-row direct variant measured 5-100 us slower: profiles/fused/).
+//
+// Mode bit 2 (modes 2/3 = 0/1 + 2): without a z neighbour (dims[2] == 1 and
+// not periodic: the 2x1x1 and 2x2x1 topologies of 2 and 4 ranks) the z-edge
+// exchange is compiled out (FEAT 195 = x/y in/out). Results are identical (207
+// skips the null z sides at run time). It pays for the 255-VGPR tiling 11
+// (loopback 2x2x1 interior rank: 0.632 vs 0.651 ms for the best 207 form) but
+// the other tilings' 195 forms measured slower than their 207 forms
+// (profiles/r1_noz/), so it is an A/B choice, not automatic.
+// XF: extra FEAT bits of the tiling (512 | 1024 for fused variant 40).
+template <typename T, int BY, int RY, int VZ, bool PF, int BZ, int XF = 0>
+void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStream_t s) {
+  const bool zx = io.in[2][0] || io.in[2][1] || io.out[2][0] || io.out[2][1];
+  if (zx || !(mode & 2)) {
+    mode &= 1;
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s);
+  } else {
+    mode &= 1;
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF>(d, io, s);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF>(d, io, s);
+  }
+}
+
+}  // namespace
+}  // namespace igg

@@ -95,6 +95,45 @@ def time_variants(T2, T, Cp, rd2, dtlam, boxes, candidates=None, reps: int = 5, 
     return {v: sorted(t)[len(t) // 2] for v, t in times.items()}
 
 
+def time_variants_pingpong(T2, T, Cp, rd2, dtlam, boxes, candidates, steps: int = 10, rounds: int = 3) -> dict:
+    """Like ``time_variants`` but in the time loop's shape: ``steps`` (even)
+    launches alternating T2 = f(T) and T = f(T2) on the model's own two
+    buffers (their HBM placement alternates exactly as in the run). T is saved
+    and restored around the measurement; T2's interior is scribbled (it is
+    overwritten by the next step anyway)."""
+    n = list(T.shape)
+    s = torch.cuda.current_stream()
+    times = {c: [] for c in candidates}
+    backup = T.clone()
+
+    def launch(c, dst, src):
+        v, gr = (c, 0) if isinstance(c, int) else c
+        native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(), boxes,
+                           True, v, s.cuda_stream, gr)
+
+    try:
+        for c in candidates:
+            launch(c, T2, T)
+            launch(c, T, T2)
+        for _ in range(rounds):
+            for c in candidates:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for k in range(steps):
+                    if k % 2 == 0:
+                        launch(c, T2, T)
+                    else:
+                        launch(c, T, T2)
+                e1.record(s)
+                e1.synchronize()
+                times[c].append(e0.elapsed_time(e1) / steps)
+    finally:
+        T.copy_(backup)
+        torch.cuda.synchronize()
+        del backup
+    return {c: sorted(t)[len(t) // 2] for c, t in times.items()}
+
+
 def autotune(T2, T, Cp, rd2, dtlam, boxes, reps: int = 5, candidates=None) -> int:
     """Fastest variant on these arrays (this process only)."""
     t = time_variants(T2, T, Cp, rd2, dtlam, boxes, candidates, reps)
