@@ -22,7 +22,7 @@ from igg._native import native  # noqa: E402
 
 
 # fused-only tilings -> the plain stencil variant with the same tiling
-PLAIN_OF = {50: 0, 41: 40}
+PLAIN_OF = {50: 0, 55: 0, 41: 40, 42: 40}
 
 
 def timed(fn, reps):

@@ -193,6 +193,28 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     __shared__ T zslots[BY * BZ * 4 * RY];
     zs = zslots + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (4 * RY);
   }
+  // FEAT 8192 (ZE): the z edge without per-row cross-lane operations. The
+  // halo values of the wave's rows are read by uniform-address loads (every
+  // lane the same address: one request per row, or scalar loads), one x step
+  // ahead, and selected into the edge lane; the edge lane's send values are
+  // kept in registers over the row loop and transposed once per step through
+  // RY LDS slots of this wave to the lane-distributed layout of the (single,
+  // coalesced) remote store. A wave with both z edges (n2 <= 64*VZ + VZ) is
+  // not supported by this form (launch_mode falls back).
+  constexpr bool ZE = (FEAT & 8192) != 0;
+  const T* zi_base = zin_lo ? zi0 : zi1;
+  T zi_cur[ZE ? RY : 1], zi_nxt[ZE ? RY : 1];
+  T* zo_lds = nullptr;
+  if constexpr (ZE) {
+    __shared__ T zo_slots[BY * BZ * RY];
+    zo_lds = zo_slots + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * RY;
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+      zi_cur[r] = T(0);
+      zi_nxt[r] = zin ? zi_base[xs * a.zp + (y0 - 1) + min(r, nv - 1)] : T(0);
+    }
+  }
+  const bool ze_lo = zin_lo && lane == 0, ze_hi = zin_hi && lane == zh;
   // Deferred sends (DF): the y row / z values of step x leave after the loads
   // of step x+1 were issued, so their acknowledgement never gates those loads.
   V ysend;
@@ -233,8 +255,17 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     // z halo of plane x (fetched one step ahead), prefetch plane x+1's. (The
     // alternative of substituting it at its use measured slower for every
     // tiling: profiles/r1_fused/feature_bisect_v11_zin_alt.log.)
-    if (zin) {
-      const T zcur = znext;
+    T zcur = T(0);
+    bool pl = false, ph = false;  // this lane patches its z=0 / z=n2-1 halo element (per row, below)
+    if constexpr (ZE) {
+#pragma unroll
+      for (int r = 0; r < RY; ++r) zi_cur[r] = zi_nxt[r];
+      if (zin && x + 1 < xe) {
+#pragma unroll
+        for (int r = 0; r < RY; ++r) zi_nxt[r] = zi_base[(x + 1) * a.zp + (y0 - 1) + min(r, nv - 1)];
+      }
+    } else if (zin) {
+      zcur = znext;
       if (x + 1 < xe) znext = zsrc[(x + 1) * a.zp];
       if constexpr ((FEAT & 4096) != 0) {
         // through the wave's LDS slots: no v_readlane -> SGPR -> VALU chain
@@ -251,16 +282,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
           }
         }
       } else {
-        // Branch-free: per-row uniform branches split the loop body into
-        // basic blocks the scheduler cannot interleave across, which at one
-        // wave per SIMD serialises the rows (profiles/r2_fused_spec/).
-        const bool pl = zin_lo && lane == 0, ph = zin_hi && lane == zh;
-#pragma unroll
-        for (int r = 0; r < RY; ++r) {
-          const T vl = lane_read(zcur, r), vh = lane_read(zcur, 32 + r);
-          tc[r][0] = pl ? vl : tc[r][0];
-          tc[r][VZ - 1] = ph ? vh : tc[r][VZ - 1];
-        }
+        pl = zin_lo && lane == 0;
+        ph = zin_hi && lane == zh;
       }
     }
     T* const xd0 = (FEAT & 64) && x == 1 ? xo0 : nullptr;
@@ -291,8 +314,21 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
       ysend_dst = nullptr;
       zsend_dst = nullptr;
     }
+    T zo_buf[ZE ? RY : 1];
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
+      if constexpr (ZE && (FEAT & 4) != 0) {
+        tc[r][0] = ze_lo ? zi_cur[r] : tc[r][0];
+        tc[r][VZ - 1] = ze_hi ? zi_cur[r] : tc[r][VZ - 1];
+      } else if constexpr ((FEAT & 4) != 0 && (FEAT & 4096) == 0) {
+        // z halo patch of row r right before its update, branch-free: patching
+        // every row up front made the step wait for all of this plane's loads
+        // at once (and per-row branches split the body into blocks the
+        // scheduler cannot interleave: profiles/r2_fused_spec/).
+        const T vl = lane_read(zcur, r), vh = lane_read(zcur, 32 + r);
+        tc[r][0] = pl ? vl : tc[r][0];
+        tc[r][VZ - 1] = ph ? vh : tc[r][VZ - 1];
+      }
       const V& c = tc[r];
       const V& yv = (r == 0) ? ym : tc[r > 0 ? r - 1 : 0];
       const V& yn = (r + 1 < nv) ? tc[(r + 1 < RY) ? r + 1 : r] : yp;
@@ -338,7 +374,9 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
           if (DF && !yrow0) { ysend = out; ysend_dst = zown ? yrow1 + x * n2 + zl : nullptr; }
           else if (zown) *reinterpret_cast<V*>(yrow1 + x * n2 + zl) = out;
         }
-        if constexpr ((FEAT & 4096) != 0) {
+        if constexpr (ZE && (FEAT & 8) != 0) {
+          zo_buf[r] = has_lo ? out[1] : out[VZ - 2];  // the send element of the edge lane
+        } else if constexpr ((FEAT & 4096) != 0) {
           if (zout_lo && lane == 0) zs[2 * RY + r] = out[1];
           if (zout_hi && lane == zh) zs[3 * RY + r] = out[VZ - 2];
         } else if constexpr ((FEAT & 8) != 0) {
@@ -351,6 +389,15 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     }
     if constexpr ((FEAT & 4096) != 0) {
       if (zdst) zv = zs[(lane < 32 ? 2 * RY : 3 * RY) + rl];
+    }
+    if constexpr (ZE && (FEAT & 8) != 0) {
+      if (zout) {  // uniform: one transpose through LDS per step
+        if (lane == (zout_lo ? 0 : zh)) {
+#pragma unroll
+          for (int r = 0; r < RY; ++r) zo_lds[r] = zo_buf[r];
+        }
+        zv = zo_lds[rl < RY ? rl : 0];
+      }
     }
     if (zdst) {
       if (DF) zsend_dst = zdst + x * a.zp;
@@ -523,6 +570,13 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
 // XF: extra FEAT bits of the tiling (512 | 1024 for fused variant 40).
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, int XF = 0>
 void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStream_t s) {
+  if constexpr ((XF & 8192) != 0) {
+    // the edge-lane z form needs every wave to hold at most one z edge
+    if (d.n[2] <= 64 * VZ + VZ) {
+      launch_mode<T, BY, RY, VZ, PF, BZ, (XF & ~8192)>(d, io, mode, s);
+      return;
+    }
+  }
   const bool zx = io.in[2][0] || io.in[2][1] || io.out[2][0] || io.out[2][1];
   if (zx || !(mode & 2)) {
     mode &= 1;

@@ -1,4 +1,4 @@
-// Fused halo-exchange diffusion kernels, tiling 11 (v2_by4_ry8) forms: fused variants 11, 40 (lane-distributed z-segment edges, one WG per CU) and 41 (+ z edge through LDS).
+// Fused halo-exchange diffusion kernels, tiling 11 (v2_by4_ry8) forms: fused variants 11, 40 (lane-distributed z-segment edges, one WG per CU) 41 (+ z edge through LDS) and 42 (+ edge-lane z exchange).
 // One translation unit per tiling family (igg/fused_impl.hpp) so they compile in parallel.
 #include "igg/fused_impl.hpp"
 
@@ -11,6 +11,7 @@ bool dispatch_t11(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode,
     case 11: launch_mode<T, 4, 8, 2, false, 1>(d, io, mode, s); break;
     case 40: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024>(d, io, mode, s); break;
     case 41: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024 | 4096>(d, io, mode, s); break;
+    case 42: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024 | 8192>(d, io, mode, s); break;  // 40 + edge-lane z
     default: return false;
   }
   return true;
