@@ -49,3 +49,23 @@ def test_failing_rank_fails_the_launch():
     assert r.returncode != 0
     assert "self-launch" in r.stderr
     assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+def test_driver_torchrun_launch_form():
+    """The driver's N-rank command (torch.distributed.run, one rank per GPU,
+    127.0.0.1 rendezvous) prints exactly one JSON line, from rank 0, with
+    n_gpus == N and not self-launched (CPU plumbing mode)."""
+    sys.path.insert(0, ROOT)
+    from tests._mp import free_port
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), BENCH,
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--device", "cpu", "--local-n", "20"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1
+    assert rec["config"]["self_launched"] is False
+    assert rec["config"]["parallelism"] == "spatial 2x1x1"
