@@ -12,7 +12,7 @@ import torch  # noqa: E402
 import igg  # noqa: E402
 from igg._native import native  # noqa: E402
 
-KINDS = {0: "triad_nt", 1: "triad", 2: "copy_nt", 3: "copy", 4: "triad_nt_u8"}
+KINDS = {0: "triad_nt", 1: "triad", 2: "copy_nt", 3: "copy", 4: "triad_nt_u8", 5: "read2_nt", 6: "write_nt"}
 
 
 def main():
@@ -33,9 +33,12 @@ def main():
             e1.record(s)
             e1.synchronize()
             ms = e0.elapsed_time(e1) / 20
-            nbytes = (3 if "triad" in name else 2) * n * 8
+            nbytes = (3 if "triad" in name else 1 if name == "write_nt" else 2) * n * 8
             res[f"{name}@{blocks}"] = {"ms": round(ms, 4), "GBs": round(nbytes / (ms * 1e-3) / 1e9, 1)}
     best = max(res.items(), key=lambda kv: kv[1]["GBs"] if "triad" in kv[0] else 0)
+    for kind in ("read2_nt", "write_nt", "copy_nt", "triad_nt"):
+        b = max(((k, v) for k, v in res.items() if k.startswith(kind + "@")), key=lambda kv: kv[1]["GBs"])
+        print(f"best {kind}: {b[0]} {b[1]['GBs']} GB/s", flush=True)
     print(json.dumps({"roofline": res, "best_triad": best}), flush=True)
 
 
