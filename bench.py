@@ -133,6 +133,12 @@ def self_launch(args) -> int:
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), IGG_BENCH_SELF_LAUNCHED="1")
+        if args.share_gpu and n > 2:
+            # Rehearsal with every rank on one GPU: N processes x 4 hardware
+            # queues oversubscribe the device's queue slots and the command
+            # processor time-slices them (8 ranks: 7.9 ms/step vs 0.25 with one
+            # queue per process, profiles/r2_reh8/). One rank per GPU never does.
+            env.setdefault("GPU_MAX_HW_QUEUES", "1")
         out = tempfile.TemporaryFile(mode="w+")
         outs.append(out)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
