@@ -123,3 +123,25 @@ def test_variants_ignore_memory_around_arrays(gpu, dtype):
                     if not err < tol:
                         bad.append((shape, v, r, len(boxes), err))
     assert not bad, bad[:10]
+
+
+def test_autotune_pingpong_stage(gpu):
+    """The model autotune's second stage re-times its front in the time loop's
+    ping-pong shape on the model's own buffers and restores T afterwards: an
+    autotuned model starts from the same state as one with a pinned variant."""
+    from igg.models.diffusion3d import PINGPONG_FRONT, Diffusion3D
+
+    igg.init_global_grid(40, 36, 72, quiet=True, init_MPI=False)
+    try:
+        m = Diffusion3D(dtype=torch.float64)
+        ref = Diffusion3D(dtype=torch.float64, variant=0)
+        pp = [k for k in m.variant_times if k.endswith("/pp")]
+        assert len(pp) == PINGPONG_FRONT
+        assert f"{m.variant}@r{m.rounds}/pp" in pp  # the pick comes from stage 2
+        assert torch.equal(m.T, ref.T)
+        m.run(4)
+        ref.run(4)
+        torch.cuda.synchronize()
+        assert torch.equal(m.T, ref.T)  # variants are bitwise interchangeable
+    finally:
+        igg.finalize_global_grid(finalize_MPI=False)

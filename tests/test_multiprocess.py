@@ -112,10 +112,16 @@ def test_gather_async_gpu(nprocs):
 @pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 0, 0), ("0", "0")),
                                                (4, (20, 22, 32, 5, 1, 1), ("9", "1")),
                                                (8, (18, 20, 40, 7, 0, 0), ("0", "1")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("11", "0"))])
+                                               (8, (16, 18, 24, 6, 1, 1), ("11", "0")),
+                                               # per-side wave classes of variant 40 and the edge-lane z
+                                               # form of 42 (n2 > 64*VZ+VZ) on one-sided (non-periodic) ranks
+                                               (4, (20, 22, 136, 5, 0, 0), ("40", "0")),
+                                               (8, (18, 20, 136, 5, 0, 1), ("42", "0"))])
 def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
     # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
+    if nprocs > 2:
+        env["GPU_MAX_HW_QUEUES"] = "1"  # ranks share one GPU: no queue oversubscription (profiles/r2_reh8/)
     run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=170)
 
 
