@@ -489,6 +489,17 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
         py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
         py::arg("stream") = 0, py::arg("rounds") = 0);
+  // Inner-box sweep through one restrict-form tiling id (fused_kernels.hip
+  // dispatch_plain), incl. the timing-probe tilings 130-132 whose results
+  // are wrong on purpose (benchmarks/refetch_probe.py).
+  m.def("diffusion3d_hx_tiling",
+        [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
+           double dtlam, int elem_bytes, int tiling, uintptr_t stream, int rounds) {
+          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes, rounds};
+          launch_diffusion3d_inner_hx(a, tiling, as_stream(stream));
+        },
+        py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
+        py::arg("elem_bytes"), py::arg("tiling"), py::arg("stream") = 0, py::arg("rounds") = 0);
   m.def("diffusion3d_fused_variant_ok", &diffusion3d_fused_variant_ok);
   m.def("fused_debug", [](uintptr_t stamps, int force_sel) {
     fused_debug(reinterpret_cast<int64_t*>(stamps), force_sel);

@@ -244,13 +244,19 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   }
   const T two = T(2);
   T evn = T(0);
-  if constexpr ((FEAT & 512) != 0) evn = t[xs * s0 + rowe];
+  // FEAT 16384 / 32768: timing probes only (results WRONG): skip the z-segment
+  // edge loads / the y-halo row loads, to price the tile-edge re-fetch.
+  if constexpr ((FEAT & 512) != 0 && (FEAT & 16384) == 0) evn = t[xs * s0 + rowe];
   for (int64_t x = xs; x < xe; ++x) {
     const int64_t off = x * s0;
     T evc = T(0);
     if constexpr ((FEAT & 512) != 0) {
       evc = evn;
-      if (x + 1 < xe) evn = t[off + s0 + rowe];
+      if constexpr ((FEAT & 16384) == 0) {
+        if (x + 1 < xe) evn = t[off + s0 + rowe];
+      } else {
+        evn = evn * T(0.5);
+      }
     }
     // z halo of plane x (fetched one step ahead), prefetch plane x+1's. (The
     // alternative of substituting it at its use measured slower for every
@@ -298,8 +304,14 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         cpn[r] = ldc(cpp + xc * s0 + rowb[r] + zl);
       }
     }
-    const V ym = vld<T, VZ>(ymb + x * yms + zl);
-    const V yp = vld<T, VZ>(ypb + x * yps + zl);
+    V ym, yp;
+    if constexpr ((FEAT & 32768) == 0) {
+      ym = vld<T, VZ>(ymb + x * yms + zl);
+      yp = vld<T, VZ>(ypb + x * yps + zl);
+    } else {
+      ym = tc[0];
+      yp = tc[RY - 1];
+    }
     T em[RY], ep[RY];
     if constexpr ((FEAT & 512) == 0) {
 #pragma unroll

@@ -41,6 +41,10 @@ void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
     case 124: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024>(d, none, s); break;
     case 125: launch_hx<T, 4, 10, 2, false, 1, false, 512 | 1024>(d, none, s); break;
     case 126: launch_hx<T, 4, 12, 2, false, 1, false, 512 | 1024>(d, none, s); break;
+    // timing probes of tiling 40 (results wrong): no z-segment edge loads / no y-halo loads / neither
+    case 130: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 16384>(d, none, s); break;
+    case 131: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 32768>(d, none, s); break;
+    case 132: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 16384 | 32768>(d, none, s); break;
     default: fail("diffusion3d (restrict form): tiling ", v, " not instantiated");
   }
 }
