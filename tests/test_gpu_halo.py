@@ -418,6 +418,29 @@ def test_gpu_bounded_sync_raises_instead_of_hanging(gpu):
     assert time.time() - t0 >= 3.5
 
 
+def test_gpu_bounded_stream_sync(gpu):
+    """The timed regions' stream wait (native event poll): raises after its
+    bound while a kernel on that stream still runs, returns promptly once it
+    is done, and costs little on an idle stream."""
+    import time
+
+    from igg import native
+    from igg.parallel.comm import bounded_stream_sync
+
+    s = torch.cuda.Stream()
+    native.gpu_spin(2.0, s.cuda_stream)
+    t0 = time.time()
+    with pytest.raises(igg.IGGError, match="did not drain"):
+        bounded_stream_sync(s.cuda_stream, timeout=0.5, what="test")
+    assert 0.4 <= time.time() - t0 < 1.9
+    bounded_stream_sync(s.cuda_stream, timeout=30.0, what="test")
+    assert time.time() - t0 >= 1.9
+    t1 = time.perf_counter()
+    for _ in range(100):
+        bounded_stream_sync(s.cuda_stream, timeout=5.0)
+    assert (time.perf_counter() - t1) / 100 < 2e-3  # microseconds in practice, generous bound
+
+
 def test_gpu_tensor_collectives_single_rank(gpu):
     igg.init_global_grid(6, 5, 4, quiet=True, init_MPI=False)
     comm = igg.get_global_grid().comm
