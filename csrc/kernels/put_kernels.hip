@@ -7,12 +7,9 @@
 namespace igg {
 namespace {
 
-__device__ __forceinline__ void store_sys(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// Relaxed system-scope store: for flag stores that follow one explicit
-// system-scope release fence (each release store would emit its own L2
-// write-back, ~1.7 us each on gfx950).
+// Relaxed system-scope store: flag stores follow one explicit system-scope
+// release fence (a release store per flag would emit its own L2 write-back,
+// ~1.7 us each on gfx950).
 __device__ __forceinline__ void store_sys_relaxed(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -372,11 +372,10 @@ void for_each_table(const std::vector<Box>& boxes, int W, int TY, bool aligned, 
     if (grp.empty()) continue;
     BoxTable bt{};
     bt.n = 0;
-    int64_t blocks = 0, tiles = 0, len_sum = 0;
+    int64_t blocks = 0, len_sum = 0;
     auto zt0 = [&](const Box& bx) { return aligned ? (bx.lo[2] / W) * W : bx.lo[2]; };
     for (const Box& bx : grp) {
       const int64_t t = ((bx.hi[2] - zt0(bx) + W - 1) / W) * ((bx.hi[1] - bx.lo[1] + TY - 1) / TY);
-      tiles += t;
       len_sum += t * (bx.hi[0] - bx.lo[0]);
     }
     // Planes per block so that sum(tiles * len0 / ch) ~= target_blocks.
