@@ -22,10 +22,15 @@ __device__ __forceinline__ uint64_t load_sys_relaxed(const uint64_t* p) {
 // is relaxed (system scope: it bypasses the caches and sees the peer's store);
 // one acquire fence after it orders the caller's later reads (an acquire load
 // per poll would invalidate the caches on every iteration).
+// Once an exchange has timed out (sticky ERROR word set), later waits give
+// up at once: a dead or diverged peer costs ONE timeout, not one per step
+// (the host reports the error at its next check and the data is invalid
+// anyway).
 __device__ bool wait_geq(const uint64_t* p, uint64_t v, const PutSync& s, uint64_t code) {
   const long long t0 = wall_clock64();
   while (load_sys_relaxed(p) < v) {
     __builtin_amdgcn_s_sleep(2);
+    if (load_sys_relaxed(s.my_flags + PutFlags::ERROR) != 0) return false;
     if (wall_clock64() - t0 > s.timeout_ticks) {
       uint64_t expected = 0;
       __hip_atomic_compare_exchange_strong(s.my_flags + PutFlags::ERROR, &expected, code, __ATOMIC_RELAXED,
