@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--gaps", default="0,4096,8192,65536,266240,1052672,2101248")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--pingpong", action="store_true",
+                    help="alternate T2=f(T) and T=f(T2) like the time loop (default: T2=f(T) only)")
+    ap.add_argument("--grid-rounds", type=int, default=0, help="grid residency rounds of each launch")
     a = ap.parse_args()
     n = a.n
     numel = n ** 3
@@ -43,9 +46,13 @@ def main():
         T.uniform_()
         Cp.fill_(1.5)
         for v in variants:
+            k = [0]
+
             def run():
-                native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], [1.0] * 3, 1e-4, 8,
-                                   [((1, 1, 1), (n - 1, n - 1, n - 1))], True, v, s.cuda_stream, 0)
+                src, dst = (T2, T) if (a.pingpong and k[0] % 2) else (T, T2)
+                k[0] += 1
+                native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), [n, n, n], [1.0] * 3, 1e-4, 8,
+                                   [((1, 1, 1), (n - 1, n - 1, n - 1))], True, v, s.cuda_stream, a.grid_rounds)
             run()
             ts = []
             for _ in range(a.rounds):
