@@ -376,18 +376,15 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
     return best, {k: round(v[0] * 1e3, 5) for k, v in times.items()}
 
 
-def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None:
-    """Fused halo exchange (stencil stores the send planes into the neighbours'
-    arenas; igg/fused.hpp) vs the schedule chosen so far: bitwise check of 24
-    steps from the same state on every rank, then A/B timing (MAX over ranks).
-    ``mode``: auto (keep the faster), on (force when it checks out), off."""
+def _fused_check(model, comm, log, nchk: int = 24) -> bool:
+    """Bitwise check of the model's CURRENT fused kernel (variant / send mode /
+    grid rounds) against the update_halo_ path: ``nchk`` steps from the same
+    state on every rank, in the timed run's execution shape (a primed arena,
+    hipGraph replays of captured fused steps plus eager steps for the parity).
+    Collective; every rank agrees. The model's state is restored."""
     import torch
 
-    if mode == "off" or not getattr(model, "can_fuse", False):
-        return None
-    # Same execution shape as the timed run: a primed arena, hipGraph replays of
-    # captured fused steps (plus eager steps for the parity), 24 steps.
-    nchk = 24
+    model.set_fused(False)
     T0, T20 = model.T.clone(), model.T2.clone()
     model.run(nchk)
     ref = model.T.clone()
@@ -404,16 +401,32 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
         _sync(comm)
         model.check()
         ok = bool(torch.equal(ref, model.T))
-    except Exception as e:  # e.g. a sync kernel timed out: the fused path does not work here
-        log(f"fused halo exchange failed its check: {type(e).__name__}: {e}"[:300])
+    except Exception as e:  # e.g. a sync kernel timed out: this fused kernel does not work here
+        log(f"fused check v{model.fused_variant}/m{model.fused_mode}/r{model.fused_rounds} failed: "
+            f"{type(e).__name__}: {e}"[:300])
+        if getattr(comm, "mesh", None) is not None:
+            comm.mesh.clear_error()
     bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
     model.T.copy_(T0)
     model.T2.copy_(T20)
+    model.fused, model._fprimed, model.graph = False, False, None  # T was restored: halos valid
     del ref, T0, T20
-    if bad != 0.0:
-        model.fused, model._fprimed, model.graph = False, False, None  # T was restored: halos valid
+    return bad == 0.0
+
+
+def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None:
+    """Fused halo exchange (stencil stores the send planes into the neighbours'
+    arenas; igg/fused.hpp) vs the schedule chosen so far: bitwise check of 24
+    steps from the same state on every rank, A/B timing of the candidates (MAX
+    over ranks), then the same bitwise check of the candidate that is kept
+    (falling back to the next fastest that passes).
+    ``mode``: auto (keep the faster), on (force when it checks out), off."""
+    if mode == "off" or not getattr(model, "can_fuse", False):
+        return None
+    if not _fused_check(model, comm, log):
         log("fused halo exchange mismatched the update_halo_ path on some rank: excluded")
         return {"fused_ok": False}
+    checked = {(model.fused_variant, model.fused_mode, model.fused_rounds)}
     # Fused kernel candidates: tiling variant x send mode (0 = stores as
     # computed, 1 = deferred one x step: robust to slow remote acknowledgements).
     # Two interleaved passes of 20 steps, best of the two per candidate: the
@@ -427,17 +440,30 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
             model.fused_variant, model.fused_mode, model.fused_rounds = v, fm, gr
             t = _timed_candidate(model, comm, 20, graph)
             times[(v, fm, gr)] = min(times.get((v, fm, gr), float("inf")), t)
-    best, t_fus = min(times.items(), key=lambda kv: kv[1])
-    model.fused_variant, model.fused_mode, model.fused_rounds = best
-    keep = mode == "on" or t_fus < t_unf
-    model.set_fused(keep)
+    model.set_fused(False)
     model.graph = None
     name = lambda k: f"v{k[0]}/m{k[1]}/r{k[2]}"  # noqa: E731
+    keep, best, rejected = False, None, []
+    for cand, t_fus in sorted(times.items(), key=lambda kv: kv[1]):
+        if not (mode == "on" or t_fus < t_unf):
+            break
+        model.fused_variant, model.fused_mode, model.fused_rounds = cand
+        if cand in checked or _fused_check(model, comm, log):
+            keep, best = True, cand
+            break
+        rejected.append(name(cand))
+    if keep:
+        model.fused_variant, model.fused_mode, model.fused_rounds = best
+    model.set_fused(keep)
+    model.graph = None
     log(f"fused A/B (ms/step): update_halo={t_unf * 1e3:.4f}, "
         + ", ".join(f"fused {name(k)}={t * 1e3:.4f}" for k, t in times.items())
-        + f" -> {'fused ' + name(best) if keep else 'update_halo'}")
+        + f" -> {'fused ' + name(best) if keep else 'update_halo'}"
+        + (f" (failed their bitwise check: {', '.join(rejected)})" if rejected else ""))
     out = {"fused_ok": True, "update_halo": round(t_unf * 1e3, 5)}
     out.update({f"fused_{name(k)}": round(t * 1e3, 5) for k, t in times.items()})
+    if rejected:
+        out["fused_rejected"] = rejected
     return out
 
 
