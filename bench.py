@@ -64,6 +64,10 @@ import time
 # store's acknowledgement is slower than in the loopback measurements.
 FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3),
                     (40, 0, 2), (42, 0, 2), (42, 1, 2), (50, 0, 2), (50, 1, 2), (50, 1, 3))
+# Direct z (send mode bit 4: the z faces go straight into the neighbours' next
+# T, no z receive code in the z-edge waves; igg/fused.hpp). Only with a z
+# neighbour (without one these equal their mode & 3 forms).
+FUSED_DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
@@ -431,12 +435,17 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
     # computed, 1 = deferred one x step: robust to slow remote acknowledgements).
     # Two interleaved passes of 20 steps, best of the two per candidate: the
     # candidates differ by a few us/step, about the size of one pass's noise.
+    cands = list(FUSED_CANDIDATES)
+    if any(model.sides[2]) and model._fh is not None and model._fh.has_fields:
+        cands += FUSED_DIRECT
+    if os.environ.get("IGG_FUSED_CANDIDATES"):  # "v/mode/rounds,..." (measurements)
+        cands = [tuple(int(x) for x in c.split("/")) for c in os.environ["IGG_FUSED_CANDIDATES"].split(",")]
     t_unf, times = float("inf"), {}
     for _ in range(2):
         model.set_fused(False)
         t_unf = min(t_unf, _timed_candidate(model, comm, 20, graph))
         model.set_fused(True)
-        for v, fm, gr in FUSED_CANDIDATES:
+        for v, fm, gr in cands:
             model.fused_variant, model.fused_mode, model.fused_rounds = v, fm, gr
             t = _timed_candidate(model, comm, 20, graph)
             times[(v, fm, gr)] = min(times.get((v, fm, gr), float("inf")), t)

@@ -521,21 +521,23 @@ PYBIND11_MODULE(_igg_native, m) {
            py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("rd2"), py::arg("dtlam"), py::arg("variant"),
            py::arg("step"), py::arg("primed"), py::arg("stream"), py::arg("rounds") = 0, py::arg("mode") = 0)
       .def("sync", [](FusedHalo& f, uintptr_t s) { f.sync(as_stream(s)); })
-      .def("io", [](FusedHalo& f, int64_t step, bool primed) {
-        const HaloIOArgs io = f.io(step, primed);
+      .def("set_fields", &FusedHalo::set_fields, py::arg("a"), py::arg("b"))
+      .def_property_readonly("has_fields", &FusedHalo::has_fields)
+      .def("io", [](FusedHalo& f, int64_t step, bool primed, uintptr_t t2, bool direct_z) {
+        const HaloIOArgs io = f.io(step, primed, t2, direct_z);
         py::list in, out;
         for (int d = 0; d < 3; ++d) {
           in.append(py::make_tuple(io.in[d][0], io.in[d][1]));
           out.append(py::make_tuple(io.out[d][0], io.out[d][1]));
         }
-        return py::make_tuple(in, out, io.zpitch);
-      })
+        return py::make_tuple(in, out, io.zpitch, io.zrow);
+      }, py::arg("step"), py::arg("primed"), py::arg("t2") = 0, py::arg("direct_z") = false)
       .def("region_offset", &FusedHalo::region_offset)
       .def_property_readonly("half_elems", &FusedHalo::half_elems)
       .def_property_readonly("zpitch", &FusedHalo::zpitch)
       .def_property_readonly("n_peers", &FusedHalo::n_peers)
       .def("check_error", [](FusedHalo& f) { f.mesh().check_error(); })
-      .def("close", [](FusedHalo& f) { f.mesh().close(); });
+      .def("close", [](FusedHalo& f) { f.close(); });
   m.def("split_boundary", [](const Int3& n, const std::array<std::array<bool, 2>, 3>& active,
                              const Int3& w) {
     std::vector<Box> slabs;

@@ -54,7 +54,12 @@ FusedHalo::FusedHalo(std::shared_ptr<PeerMesh> mesh, const std::array<int64_t, 3
   sync_.timeout_ticks = mesh_->timeout_ticks();
 }
 
-HaloIOArgs FusedHalo::io(int64_t step, bool primed) const {
+void FusedHalo::set_fields(uintptr_t a, uintptr_t b) {
+  if (!a || !b || a == b) fail("FusedHalo.set_fields: two distinct field buffers expected");
+  fields_ = mesh_->map_buffers({a, b});  // collective
+}
+
+HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z) const {
   HaloIOArgs io{};
   const int64_t eb = elem_;
   const int64_t wh = (step & 1) * half_, rh = ((step + 1) & 1) * half_;
@@ -68,6 +73,26 @@ HaloIOArgs FusedHalo::io(int64_t step, bool primed) const {
       if (primed) io.in[d][s] = reinterpret_cast<uintptr_t>(mine + (rh + off_[d][s]) * eb);
     }
   io.zpitch = zp_;
+  if (direct_z && (nb_[2][0] != PROC_NULL || nb_[2][1] != PROC_NULL)) {
+    if (fields_.empty()) fail("FusedHalo: direct z needs the field buffers (set_fields)");
+    const char* mine_t2 = reinterpret_cast<const char*>(t2);
+    int k = -1;
+    for (int i = 0; i < 2; ++i)
+      if (fields_[mesh_->rank()][i] == mine_t2) k = i;
+    if (k < 0) fail("FusedHalo: direct z: the output field is not one of the registered buffers");
+    const int64_t n1 = n_[1], n2 = n_[2];
+    for (int s = 0; s < 2; ++s) {
+      const int r = nb_[2][s];
+      io.in[2][s] = 0;
+      if (r == PROC_NULL) continue;
+      // My z=1 (side 0) is the neighbour's z=n2-1 halo, my z=n2-2 its z=0;
+      // + n2 absorbs the kernel's (y-1) row index.
+      const int64_t col = (s == 0 ? n2 - 1 : 0) + n2;
+      io.out[2][s] = reinterpret_cast<uintptr_t>(fields_.at(r).at(k) + col * eb);
+    }
+    io.zpitch = n1 * n2;
+    io.zrow = n2;
+  }
   return io;
 }
 
@@ -76,7 +101,7 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
   for (int d = 0; d < 3; ++d)
     if (a.n[d] != n_[d]) fail("FusedHalo.step: field shape does not match the fused halo's local grid");
   if (a.elem_bytes != elem_) fail("FusedHalo.step: field dtype does not match the fused halo");
-  launch_diffusion3d_fused(a, io(step, primed), variant, mode, stream);
+  launch_diffusion3d_fused(a, io(step, primed, a.t2, (mode & 4) != 0), variant, mode, stream);
   sync(stream);
 }
 

@@ -16,12 +16,20 @@
 // the per-step neighbour barrier of the sync kernel bounds the skew to one.
 // The fields' own halo planes are not touched; sync_halo (update_halo_ of T)
 // materialises them when a caller needs them (gather, output, mode switch).
+// Direct z (mode bit 4, set_fields): the z faces skip the arena and land in
+// the halo column of the neighbour's next field, which the neighbour's next
+// step reads like any other element. Safe for the same reason as the arena:
+// a neighbour writes my buffer k (halo elements only) during the step in
+// which my stencil writes buffer k's interior and reads buffer 1-k; my
+// previous step (which read buffer k) finished before that neighbour's sync
+// kernel let it start this step.
 // Results are bitwise identical to stencil + update_halo_ (tests/test_fused.py).
 #pragma once
 
 #include <array>
 #include <cstdint>
 #include <memory>
+#include <vector>
 
 #include <hip/hip_runtime_api.h>
 
@@ -40,8 +48,17 @@ class FusedHalo {
             const std::array<std::array<int, 2>, 3>& nb);
 
   // Arena regions of the step with counter `step` (writes half step&1; reads
-  // half (step-1)&1 if `primed`, else the field's own halo planes).
-  HaloIOArgs io(int64_t step, bool primed) const;
+  // half (step-1)&1 if `primed`, else the field's own halo planes). With
+  // `direct_z`, the z sends target the halo column of the neighbour's buffer
+  // that corresponds to `t2` (set_fields) and nothing is read from the arena
+  // along z.
+  HaloIOArgs io(int64_t step, bool primed, uintptr_t t2 = 0, bool direct_z = false) const;
+  // Collective: the two ping-pong field buffers of this rank (same order on
+  // every rank, registered at the same step); needed by direct z (mode bit 4).
+  // Every rank swaps them in lockstep, so "my t2 is buffer k" means "each
+  // neighbour's t2 is its buffer k".
+  void set_fields(uintptr_t a, uintptr_t b);
+  bool has_fields() const { return !fields_.empty(); }
   // Stencil with fused send/receive + sync kernel, on `stream`.
   void step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed, hipStream_t stream);
   // Fill the shape/dtype of `a` from this halo's local grid.
@@ -57,6 +74,10 @@ class FusedHalo {
   int64_t zpitch() const { return zp_; }
   int n_peers() const { return sync_.n_out; }
   PeerMesh& mesh() { return *mesh_; }
+  void close() {
+    fields_.clear();
+    mesh_->close();
+  }
 
  private:
   std::shared_ptr<PeerMesh> mesh_;
@@ -66,6 +87,7 @@ class FusedHalo {
   int64_t off_[3][2];
   int64_t half_ = 0, zp_ = 0;
   PutSync sync_{};
+  std::vector<std::vector<char*>> fields_;  // [rank][k]: ping-pong buffer k (set_fields)
 };
 
 }  // namespace igg

@@ -75,7 +75,7 @@ __device__ __forceinline__ int64_t hx_chunk(int64_t cxr, int64_t nch) {
 
 template <typename T>
 struct HxScal {
-  int64_t n0, n1, n2, zp;
+  int64_t n0, n1, n2, zp, zrow;  // z sends: x*zp + (y-1)*zrow (arena: zrow 1; direct: n1*n2, n2)
   int64_t ntz, nty, ch;  // z tiles, y tiles, planes per chunk
   T rdx2, rdy2, rdz2, dtlam;
   // Diagnostics (fused_debug): per-wave {class, start, end, cu} stamps
@@ -180,7 +180,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   const T* zsrc = lo_l && zin_lo ? zi0 + (y0 - 1) + rl
                                  : (hi_l && zin_hi ? zi1 + (y0 - 1) + rl
                                                    : (zin_lo ? zi0 : zi1) + (y0 - 1));
-  T* zdst = lo_l && zout_lo ? zo0 + (y0 - 1) + rl : (hi_l && zout_hi ? zo1 + (y0 - 1) + rl : nullptr);
+  const int64_t zro = ((y0 - 1) + rl) * a.zrow;
+  T* zdst = lo_l && zout_lo ? zo0 + zro : (hi_l && zout_hi ? zo1 + zro : nullptr);
   const bool remote = zout || yrow0 || yrow1 || (xs == 1 && xo0) || (xe == n0 - 1 && xo1);
   T znext = T(0), zv = T(0);
   if (zin) znext = zsrc[xs * a.zp];
@@ -537,7 +538,7 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
   const int block = 64 * BY * BZ;
   constexpr int W = 64 * VZ * BZ, TY = BY * RY;
   HxScal<T> a;
-  a.n0 = n0; a.n1 = n1; a.n2 = n2; a.zp = io.zpitch;
+  a.n0 = n0; a.n1 = n1; a.n2 = n2; a.zp = io.zpitch; a.zrow = io.zrow > 0 ? io.zrow : 1;
   a.ntz = (n2 - 1 + W - 1) / W;
   a.nty = (n1 - 2 + TY - 1) / TY;
   const int64_t len0 = n0 - 2, tiles = a.ntz * a.nty;
@@ -579,6 +580,12 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
 // (loopback 2x2x1 interior rank: 0.632 vs 0.651 ms for the best 207 form) but
 // the other tilings' 195 forms measured slower than their 207 forms
 // (profiles/r1_noz/), so it is an A/B choice, not automatic.
+//
+// Mode bit 4 (direct z, FusedHalo with registered field buffers): the z-face
+// values are stored straight into the halo column of the neighbour's next
+// field (one element per row, the row's own 64-B line) instead of a packed
+// arena region, so no wave patches a received z halo into its rows (the cost
+// of the z-edge waves of tilings 11/40: profiles/r2_fused_spec/).
 // XF: extra FEAT bits of the tiling (512 | 1024 for fused variant 40).
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, int XF = 0>
 void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStream_t s) {
@@ -590,7 +597,14 @@ void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStre
     }
   }
   const bool zx = io.in[2][0] || io.in[2][1] || io.out[2][0] || io.out[2][1];
-  if (zx || !(mode & 2)) {
+  if ((mode & 4) && zx) {
+    // Direct z (FEAT 203 = 207 without z-in): the z sends land in the
+    // receivers' field halo elements, so the z-edge waves read their halo
+    // from the field like every other wave and carry only the send code.
+    if (io.in[2][0] || io.in[2][1]) fail("diffusion3d (fused halo): direct z mode with z arena input");
+    if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF>(d, io, s);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF>(d, io, s);
+  } else if (zx || !(mode & 2)) {
     mode &= 1;
     if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s);
     else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s);

@@ -52,6 +52,12 @@ class PeerMesh {
   void check_error() const;
   void clear_error();
   int64_t timeout_ticks() const { return timeout_ticks_; }
+  // Collective: maps device buffers of every rank (each rank passes its own
+  // pointers, the same count everywhere; pointers may lie inside larger
+  // allocations, e.g. torch's). Returns out[r][i] = rank r's buffer i in this
+  // process (this rank's own pointers as given). The mappings live until
+  // close(); mapping again replaces them.
+  std::vector<std::vector<char*>> map_buffers(const std::vector<uintptr_t>& mine);
   // Collective teardown (also run by the destructor without the collectives).
   void close();
 
@@ -64,6 +70,8 @@ class PeerMesh {
   size_t arena_bytes_ = 0;
   std::vector<uint64_t*> peer_flags_;
   std::vector<char*> peer_arena_;
+  std::vector<void*> mapped_;  // map_buffers() mappings (one per distinct peer allocation)
+  void unmap_buffers();
   int64_t timeout_ticks_ = 0;
   // Fine-grained (coherent across devices; reads cached in L2 within a kernel,
   // invalidated at kernel-boundary acquires): the fused stencil's halo reads

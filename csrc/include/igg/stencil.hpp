@@ -51,12 +51,16 @@ void launch_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes, i
 // receiver at that side) and takes its face halos from its own arena regions
 // (`in`, 0 = read the field's halo planes). Region layouts (elements):
 //   dim 0 faces [n1][n2], dim 1 faces [n0][n2], dim 2 faces [n0][zpitch]
-//   (index x*zpitch + (y-1)). Needs a vector variant (fused_variant_ok) and
-//   n2 % vz == 0.
+//   (index x*zpitch + (y-1)*zrow, zrow 0 meaning 1). Needs a vector variant
+//   (fused_variant_ok) and n2 % vz == 0. Direct z (mode bit 4): the z sends
+//   go straight into the halo elements of the receiver's next field
+//   (zpitch = n1*n2, zrow = n2, `out` offset to the halo column), and no
+//   z receive code is compiled (`in[2]` must be 0).
 struct HaloIOArgs {
   uintptr_t in[3][2];
   uintptr_t out[3][2];
   int64_t zpitch;
+  int64_t zrow;
 };
 bool diffusion3d_fused_variant_ok(int v);
 // Diagnostics of the fused kernel: per-wave {feature class, start, end, hw id}
@@ -68,7 +72,8 @@ void fused_debug(int64_t* stamps, int force_sel);
 // (tiling = a fused-capable variant index); used by the "hx" variants.
 void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t stream);
 // mode 0: sends stored as computed; 1: deferred one x step; + 2: z-edge exchange
-// compiled out when there is no z neighbour (see fused_kernels.hip).
+// compiled out when there is no z neighbour; + 4: direct z (see HaloIOArgs and
+// fused_impl.hpp launch_mode).
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
                               hipStream_t stream);
 void host_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes);

@@ -6,7 +6,9 @@
 #include "igg/ipc.hpp"
 
 #include <cstdlib>
+#include <cstring>
 #include <ios>
+#include <map>
 
 namespace igg {
 
@@ -57,6 +59,8 @@ PeerMesh::~PeerMesh() {
     peer_arena_[r] = nullptr;
     peer_flags_[r] = nullptr;
   }
+  for (void* p : mapped_) (void)hipIpcCloseMemHandle(p);
+  mapped_.clear();
   if (arena_) (void)hipFree(arena_);
   if (flags_) (void)hipFree(flags_);
   if (side_) (void)hipStreamDestroy(side_);
@@ -116,10 +120,75 @@ void PeerMesh::ensure_arena(size_t bytes) {
   exchange_handles(false);
 }
 
+void PeerMesh::unmap_buffers() {
+  for (void* p : mapped_) ipc_close(p);
+  mapped_.clear();
+}
+
+std::vector<std::vector<char*>> PeerMesh::map_buffers(const std::vector<uintptr_t>& mine) {
+  if (closed_) fail("PeerMesh: used after close()");
+  // Old mappings go first: every rank drains its work into them, then agrees.
+  if (!mapped_.empty()) {
+    IGG_HIP_CHECK(hipDeviceSynchronize());
+    (void)allgather_(std::string());
+    unmap_buffers();
+  }
+  // Record per buffer: handle of its allocation + offset inside it.
+  const size_t hb = sizeof(hipIpcMemHandle_t);
+  std::string rec;
+  if (nranks_ > 1)
+    for (uintptr_t p : mine) {
+      void* base = nullptr;
+      size_t size = 0;
+      IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(p)));
+      const uint64_t off = p - reinterpret_cast<uintptr_t>(base);
+      rec += ipc_get_handle(base);
+      rec.append(reinterpret_cast<const char*>(&off), 8);
+    }
+  const std::vector<std::string> all = allgather_(rec);
+  if (static_cast<int>(all.size()) != nranks_) fail("PeerMesh: allgather returned ", all.size(), " entries");
+  std::vector<std::vector<char*>> out(nranks_);
+  std::string error;
+  try {
+    for (int r = 0; r < nranks_; ++r) {
+      if (r == rank_) {
+        for (uintptr_t p : mine) out[r].push_back(reinterpret_cast<char*>(p));
+        continue;
+      }
+      const std::string& h = all[r];
+      if (h.size() != mine.size() * (hb + 8)) fail("PeerMesh.map_buffers: rank ", r, " passed a different count");
+      // One mapping per distinct allocation (two buffers of one allocation
+      // share a handle; opening a handle twice in a process is not allowed).
+      std::map<std::string, char*> opened;
+      for (size_t i = 0; i < mine.size(); ++i) {
+        const std::string key = h.substr(i * (hb + 8), hb);
+        uint64_t off = 0;
+        std::memcpy(&off, h.data() + i * (hb + 8) + hb, 8);
+        auto it = opened.find(key);
+        if (it == opened.end()) {
+          char* base = static_cast<char*>(ipc_open(key));
+          mapped_.push_back(base);
+          it = opened.emplace(key, base).first;
+        }
+        out[r].push_back(it->second + off);
+      }
+    }
+  } catch (const Error& e) {
+    error = e.what();
+  }
+  const std::vector<std::string> status = allgather_(error.empty() ? std::string("1") : std::string("0"));
+  for (int r = 0; r < static_cast<int>(status.size()); ++r)
+    if (status[r] != "1")
+      fail("PeerMesh: rank ", r, " could not map the peers' buffers",
+           error.empty() ? std::string() : std::string(" (here: ") + error + ")");
+  return out;
+}
+
 void PeerMesh::close() {
   if (closed_) return;
   IGG_HIP_CHECK(hipDeviceSynchronize());
   (void)allgather_(std::string());
+  unmap_buffers();
   for (int r = 0; r < nranks_; ++r) {
     if (r == rank_) continue;
     if (peer_arena_[r]) ipc_close(peer_arena_[r]);

@@ -31,6 +31,7 @@ bitwise identical to the update_halo_ path.
 from __future__ import annotations
 
 import math
+import warnings
 
 import torch
 
@@ -138,7 +139,8 @@ class Diffusion3D:
         self.fused = False
         # Fused kernel: variant (tiling; one with a fused instantiation) and
         # send mode (0 stores as computed, 1 deferred one x step; +2 compiles the
-        # z-edge exchange out when there is no z neighbour).
+        # z-edge exchange out when there is no z neighbour; +4 direct z: the z
+        # faces go straight into the neighbours' next T, no z receive code).
         self.fused_variant = 0
         self.fused_mode = 0
         self.fused_rounds = 3  # grid residency rounds (profiles/r1_fused/grid.log)
@@ -169,6 +171,12 @@ class Diffusion3D:
         if flag:
             if self._fh is None:
                 self._fh = _make_fused_halo(self)
+                try:  # direct z sends (fused_mode bit 4) write into the neighbours' T/T2
+                    self._fh.set_fields(self.T.data_ptr(), self.T2.data_ptr())
+                except Exception as e:  # collective outcome: every rank gets here together
+                    warnings.warn(f"Diffusion3D: direct z sends unavailable ({e})")
+            if self.fused_mode & 4 and not self._fh.has_fields:
+                self.fused_mode &= 3
             if not stencil.native.diffusion3d_fused_variant_ok(int(self.fused_variant)):
                 self.fused_variant = 0
             self.set_overlap(False)

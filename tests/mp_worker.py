@@ -147,7 +147,9 @@ def scenario_diffusion_fused(nx, ny, nz, steps, periodic, graph):
     a = Diffusion3D(dtype=torch.float64, device=device, variant=v)
     b = Diffusion3D(dtype=torch.float64, device=device, variant=v)
     b.fused_variant, b.fused_mode = v, int(os.environ.get("IGG_TEST_FUSED_MODE", "0"))
+    want = b.fused_mode
     assert b.set_fused(True), "fused mode unavailable"
+    assert b.fused_mode == want, f"send mode {want} unavailable (direct z needs the peers' field buffers)"
     a.run(steps)
     if int(graph):
         b.step()

@@ -96,6 +96,43 @@ def test_fused_no_z_exchange_matches_update_halo(gpu, variant, dtype, mode, peri
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [4, 5])
+@pytest.mark.parametrize("variant", [0, 2, 9, 11, 14, 40, 41, 42, 50])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("periods", [(1, 1, 1), (0, 0, 1), (1, 0, 1)])
+def test_fused_direct_z_matches_update_halo(gpu, variant, dtype, mode, periods):
+    """Modes 4/5 (direct z): the z faces are stored into the halo column of the
+    neighbour's next field (here: this rank's own, periodic) and no z receive
+    code runs; same results as update_halo_, halos included after sync_halo."""
+    a, b = _pair((34, 29, 136), periods, dtype, variant, mode=mode)
+    assert b.fused_mode == mode
+    a.run(9)
+    b.run(9)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_fused_direct_z_graph(gpu):
+    """Direct z under hipGraph replays (both buffer parities captured) and the
+    loopback emulation's remote path."""
+    a, b = _pair((40, 36, 72), (1, 1, 1), torch.float64, 42, loopback=True, mode=4)
+    a.run(3)
+    b.run(3)
+    b.capture(steps=4)
+    a.run(11)
+    b.run(11)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
 def test_fused_loopback_graph_and_mode_switches(gpu):
     """Loopback grid, hipGraph replays with odd/even step counts, sync_halo in
     between (re-primes from the field) and switching back to update_halo_."""
@@ -134,11 +171,22 @@ def test_fused_arena_layout(gpu):
     for d in range(3):
         for s in range(2):
             assert (fh.region_offset(d, s) * 8) % 256 == 0
-    ins, outs, zp = fh.io(0, False)
+    ins, outs, zp, zr = fh.io(0, False)
     assert all(p == 0 for pair in ins for p in pair)  # unprimed: halos from the field
-    ins, outs, zp = fh.io(1, True)
+    ins, outs, zp, zr = fh.io(1, True)
     assert all(p != 0 for pair in ins for p in pair) and all(p != 0 for pair in outs for p in pair)
     assert fh.n_peers == 1
+    # direct z: the z sends target the halo columns of the buffer matching t2
+    assert fh.has_fields
+    n1, n2, eb = 37, 64, 8
+    for t2 in (b.T2, b.T):
+        ins, outs, zp, zr = fh.io(1, True, t2.data_ptr(), True)
+        assert ins[2] == (0, 0) and ins[0][0] != 0
+        assert zp == n1 * n2 and zr == n2
+        assert outs[2][0] == t2.data_ptr() + (n2 - 1 + n2) * eb  # self-periodic: my own next field
+        assert outs[2][1] == t2.data_ptr() + n2 * eb
+    with pytest.raises(Exception, match="registered"):
+        fh.io(1, True, b.Cp.data_ptr(), True)
     igg.finalize_global_grid(finalize_MPI=False)
 
 

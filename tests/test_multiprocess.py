@@ -116,7 +116,11 @@ def test_gather_async_gpu(nprocs):
                                                # per-side wave classes of variant 40 and the edge-lane z
                                                # form of 42 (n2 > 64*VZ+VZ) on one-sided (non-periodic) ranks
                                                (4, (20, 22, 136, 5, 0, 0), ("40", "0")),
-                                               (8, (18, 20, 136, 5, 0, 1), ("42", "0"))])
+                                               (8, (18, 20, 136, 5, 0, 1), ("42", "0")),
+                                               # direct z (mode bit 4): z faces into the neighbours' T2
+                                               (2, (24, 20, 64, 6, 1, 0), ("40", "4")),
+                                               (8, (18, 20, 136, 5, 0, 1), ("42", "4")),
+                                               (8, (16, 18, 24, 6, 1, 1), ("0", "5"))])
 def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
     # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
@@ -126,7 +130,7 @@ def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nprocs,kernel", [(4, ("0", "0")), (8, ("0", "1"))])
+@pytest.mark.parametrize("nprocs,kernel", [(4, ("0", "0")), (8, ("0", "1")), (8, ("40", "4"))])
 def test_fused_soak_with_rank_skew(nprocs, kernel):
     """Thousands of graph-replayed fused steps with random host skew between
     ranks stay bitwise equal to stencil + update_halo_."""
