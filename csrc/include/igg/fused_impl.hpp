@@ -102,6 +102,14 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
          T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T>& a) {
   using V = typename Vec<T, VZ>::type;
   constexpr int W = 64 * VZ * BZ;
+  // FEAT 65536 (RV, plain sweeps only): reversed march - chunks from the top x
+  // down and each chunk's planes from high x to low - for every other step of
+  // the ping-pong loop, so a step starts on the planes the previous (forward)
+  // step touched last, which may still sit in the memory-side Infinity Cache.
+  // The x term is summed in the forward order: results are bitwise identical.
+  constexpr bool RV = (FEAT & 65536) != 0;
+  static_assert(!RV || (FEAT & (1 | 2 | 4 | 8 | 64 | 128 | 4096 | 8192)) == 0, "RV: plain sweeps only");
+  constexpr int64_t DX = RV ? -1 : 1;
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t tz = b % a.ntz;
   const int64_t rest = b / a.ntz;
@@ -112,7 +120,7 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   // instead of at the kernel's tail. Scheduling only: results are unchanged.
   const int64_t nch = (a.n0 - 2 + a.ch - 1) / a.ch;
   const int64_t cxr = rest / a.nty;
-  const int64_t cx = hx_chunk(cxr, nch);
+  const int64_t cx = RV ? nch - 1 - cxr : hx_chunk(cxr, nch);
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wz = wid % BZ, wy = wid / BZ;
@@ -235,26 +243,29 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     if constexpr ((FEAT & 256) != 0) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
     return vld<T, VZ>(p);
   };
+  // tm / tp: the planes behind / ahead of the march (x - DX / x + DX)
+  const int64_t xf = RV ? xe - 1 : xs, len = xe - xs;
   V tm[RY], tc[RY], tp[RY], cp[RY];
 #pragma unroll
   for (int r = 0; r < RY; ++r) {
-    tm[r] = vld<T, VZ>(plane(xs - 1) + rowb[r] + zl);
-    tc[r] = vld<T, VZ>(plane(xs) + rowb[r] + zl);
-    tp[r] = vld<T, VZ>(plane(xs + 1) + rowb[r] + zl);
-    cp[r] = ldc(cpp + xs * s0 + rowb[r] + zl);
+    tm[r] = vld<T, VZ>(plane(xf - DX) + rowb[r] + zl);
+    tc[r] = vld<T, VZ>(plane(xf) + rowb[r] + zl);
+    tp[r] = vld<T, VZ>(plane(xf + DX) + rowb[r] + zl);
+    cp[r] = ldc(cpp + xf * s0 + rowb[r] + zl);
   }
   const T two = T(2);
   T evn = T(0);
   // FEAT 16384 / 32768: timing probes only (results WRONG): skip the z-segment
   // edge loads / the y-halo row loads, to price the tile-edge re-fetch.
-  if constexpr ((FEAT & 512) != 0 && (FEAT & 16384) == 0) evn = t[xs * s0 + rowe];
-  for (int64_t x = xs; x < xe; ++x) {
+  if constexpr ((FEAT & 512) != 0 && (FEAT & 16384) == 0) evn = t[xf * s0 + rowe];
+  int64_t x = xf;
+  for (int64_t i = 0; i < len; ++i, x += DX) {
     const int64_t off = x * s0;
     T evc = T(0);
     if constexpr ((FEAT & 512) != 0) {
       evc = evn;
       if constexpr ((FEAT & 16384) == 0) {
-        if (x + 1 < xe) evn = t[off + s0 + rowe];
+        if (i + 1 < len) evn = t[off + DX * s0 + rowe];
       } else {
         evn = evn * T(0.5);
       }
@@ -297,7 +308,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     T* const xd1 = (FEAT & 64) && x == n0 - 2 ? xo1 : nullptr;
     V tn[RY], cpn[RY];
     if (PF) {
-      const int64_t xn = min(x + 2, n0 - 1), xc = min(x + 1, xe - 1);
+      const int64_t xn = RV ? max<int64_t>(x - 2, 0) : min(x + 2, n0 - 1);
+      const int64_t xc = RV ? max<int64_t>(x - 1, xs) : min(x + 1, xe - 1);
       const T* pn = ((FEAT & 1) && xn == n0 - 1 && xi1) ? xi1 : t + xn * s0;
 #pragma unroll
       for (int r = 0; r < RY; ++r) {
@@ -361,14 +373,18 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         const T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
         const T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
         const T c2 = two * c[e];
-        const T lap = (tp[r][e] - c2 + tm[r][e]) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
+        const T xpv = RV ? tm[r][e] : tp[r][e], xmv = RV ? tp[r][e] : tm[r][e];  // planes x+1, x-1
+        const T lap = (xpv - c2 + xmv) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
                       (zp - c2 + zm) * a.rdz2;
         out[e] = c[e] + a.dtlam / cp[r][e] * lap;
       }
       if (r < nv) {
         T* dst = t2 + off + rowb[r] + zl;
         if (lane_full) {
-          __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
+          // FEAT 131072: plain (temporal) stores, to measure what the
+          // non-temporal hint costs or saves in the Infinity Cache
+          if constexpr ((FEAT & 131072) != 0) *reinterpret_cast<V*>(dst) = out;
+          else __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
         } else {
 #pragma unroll
           for (int e = 0; e < VZ; ++e)
@@ -425,12 +441,12 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         cp[r] = cpn[r];
       }
     }
-    if (!PF && x + 1 < xe) {
-      const T* pn = ((FEAT & 1) && x + 2 == n0 - 1 && xi1) ? xi1 : t + (x + 2) * s0;
+    if (!PF && i + 1 < len) {
+      const T* pn = ((FEAT & 1) && x + 2 == n0 - 1 && xi1) ? xi1 : t + (x + 2 * DX) * s0;
 #pragma unroll
       for (int r = 0; r < RY; ++r) {
         tp[r] = vld<T, VZ>(pn + rowb[r] + zl);
-        cp[r] = ldc(cpp + (x + 1) * s0 + rowb[r] + zl);
+        cp[r] = ldc(cpp + (x + DX) * s0 + rowb[r] + zl);
       }
     }
   }

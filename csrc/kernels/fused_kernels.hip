@@ -45,6 +45,14 @@ void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
     case 130: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 16384>(d, none, s); break;
     case 131: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 32768>(d, none, s); break;
     case 132: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 16384 | 32768>(d, none, s); break;
+    // reversed march (FEAT 65536) of tilings 0, 11, 100, 124 (= id + 200)
+    case 200: launch_hx<T, 4, 4, 4, false, 1, false, 65536>(d, none, s); break;
+    case 211: launch_hx<T, 4, 8, 2, false, 1, false, 65536>(d, none, s); break;
+    case 300: launch_hx<T, 2, 8, 2, false, 1, false, 65536>(d, none, s); break;
+    case 324: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 65536>(d, none, s); break;
+    // tiling 11 with temporal T2 stores (FEAT 131072), forward / reversed
+    case 411: launch_hx<T, 4, 8, 2, false, 1, false, 131072>(d, none, s); break;
+    case 611: launch_hx<T, 4, 8, 2, false, 1, false, 131072 | 65536>(d, none, s); break;
     default: fail("diffusion3d (restrict form): tiling ", v, " not instantiated");
   }
 }
