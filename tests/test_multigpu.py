@@ -89,7 +89,12 @@ def test_diffusion_8_ranks_matches_global(transport):
 @pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 0, 0), ("0", "0")),
                                                (4, (20, 22, 32, 5, 1, 1), ("9", "1")),
                                                (8, (18, 20, 40, 7, 0, 0), ("0", "1")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("11", "0"))])
+                                               (8, (16, 18, 24, 6, 1, 1), ("11", "0")),
+                                               # direct z (mode bit 4): z faces stored over xGMI into
+                                               # the halo column of the neighbour's next field
+                                               (2, (24, 20, 64, 6, 1, 0), ("40", "4")),
+                                               (8, (18, 20, 136, 5, 0, 1), ("42", "4")),
+                                               (8, (16, 18, 24, 6, 1, 1), ("0", "5"))])
 def test_fused_exchange_across_devices(nprocs, cfg, kernel):
     """Stencil kernel stores its send planes into the neighbours' arenas over
     xGMI: bitwise equal to stencil + update_halo_ (RCCL) on every rank."""
@@ -98,10 +103,10 @@ def test_fused_exchange_across_devices(nprocs, cfg, kernel):
     run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=170)
 
 
-@pytest.mark.parametrize("nprocs", [4, 8])
-def test_fused_soak_across_devices(nprocs):
+@pytest.mark.parametrize("nprocs,kernel", [(4, ("0", "1")), (8, ("0", "1")), (8, ("40", "4"))])
+def test_fused_soak_across_devices(nprocs, kernel):
     need(nprocs)
-    env = {**PUT, "IGG_PUT_TIMEOUT": "30", "IGG_TEST_VARIANT": "0", "IGG_TEST_FUSED_MODE": "1"}
+    env = {**PUT, "IGG_PUT_TIMEOUT": "30", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
     run_ranks(nprocs, "fused_soak", 20, 18, 32, 40, 40, env_extra=env, timeout=170)
 
 
