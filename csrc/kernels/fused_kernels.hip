@@ -45,6 +45,15 @@ void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
     case 130: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 16384>(d, none, s); break;
     case 131: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 32768>(d, none, s); break;
     case 132: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | 16384 | 32768>(d, none, s); break;
+    // full-row z tiles (W = 64*VZ*BZ = 512 points: no z-segment edge re-fetch
+    // between workgroups; the edge values of inner waves come from a sibling
+    // wave's lines on the same CU)
+    case 140: launch_hx<T, 4, 8, 2, false, 4, false, 0>(d, none, s); break;
+    case 141: launch_hx<T, 2, 8, 2, false, 4, false, 0>(d, none, s); break;
+    case 142: launch_hx<T, 4, 4, 2, false, 4, false, 0>(d, none, s); break;
+    case 143: launch_hx<T, 4, 4, 4, false, 2, false, 0>(d, none, s); break;
+    case 144: launch_hx<T, 4, 8, 4, false, 2, false, 0>(d, none, s); break;
+    case 145: launch_hx<T, 2, 8, 2, false, 4, false, 512>(d, none, s); break;
     // reversed march (FEAT 65536) of tilings 0, 11, 100, 124 (= id + 200)
     case 200: launch_hx<T, 4, 4, 4, false, 1, false, 65536>(d, none, s); break;
     case 211: launch_hx<T, 4, 8, 2, false, 1, false, 65536>(d, none, s); break;
