@@ -68,6 +68,9 @@ FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 
 # T, no z receive code in the z-edge waves; igg/fused.hpp). Only with a z
 # neighbour (without one these equal their mode & 3 forms).
 FUSED_DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
+# f32 (1024^3 config): tiling 14 with the edge-lane z exchange (fused variant
+# 44) is the fastest fused form there (profiles/r2_f32_fused/).
+FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
@@ -438,6 +441,8 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
     cands = list(FUSED_CANDIDATES)
     if any(model.sides[2]) and model._fh is not None and model._fh.has_fields:
         cands += FUSED_DIRECT
+        if model.T.dtype.itemsize == 4:
+            cands += FUSED_DIRECT_F32
     if os.environ.get("IGG_FUSED_CANDIDATES"):  # "v/mode/rounds,..." (measurements)
         cands = [tuple(int(x) for x in c.split("/")) for c in os.environ["IGG_FUSED_CANDIDATES"].split(",")]
     t_unf, times = float("inf"), {}

@@ -12,7 +12,7 @@ force_sel runs every wave with one class (timing only: 0 on an exchanging
 grid skips its exchange): 'auto' vs 'all0' separates the cost of the boundary
 waves' work from the cost of merely having the exchange code in the kernel.
 
-Usage: python benchmarks/fused_waves.py [--n 512] [--variants 40,0] [--rounds 2] [--mode 0]
+Usage: python benchmarks/fused_waves.py [--n 512] [--variants 40,0] [--rounds 2] [--mode 0] [--dtype float64]
 """
 import argparse
 import os
@@ -25,7 +25,7 @@ import torch  # noqa: E402
 import igg  # noqa: E402
 from igg._native import native  # noqa: E402
 
-PLAIN_OF = {50: 0, 55: 0, 41: 40, 42: 40}
+PLAIN_OF = {50: 0, 55: 0, 41: 40, 42: 40, 44: 14, 45: 0}
 
 
 def main():
@@ -35,10 +35,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
     a = ap.parse_args()
     n = a.n
     igg.init_global_grid(n, n, n, periodx=1, periody=1, periodz=1, quiet=True)
-    dt = torch.float64
+    dt = getattr(torch, a.dtype)
     T = torch.rand(n, n, n, dtype=dt, device="cuda")
     T2 = T.clone()
     Cp = torch.rand(n, n, n, dtype=dt, device="cuda") + 1
@@ -49,6 +50,8 @@ def main():
     mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
     fh6 = native.FusedHalo(mesh, [n, n, n], eb, [[0, 0], [0, 0], [0, 0]])
     fh0 = native.FusedHalo(mesh, [n, n, n], eb, [[-1, -1], [-1, -1], [-1, -1]])
+    if a.mode & 4:  # direct z: the z sends land in the halo column of the other buffer
+        fh6.set_fields(T.data_ptr(), T2.data_ptr())
     stamps = torch.zeros(1 << 22, dtype=torch.int64, device="cuda")
     k = [0]
 
@@ -69,7 +72,7 @@ def main():
             ts.append(e0.elapsed_time(e1) / a.reps)
         return sorted(ts)[1]
 
-    print(f"n={n}^3 f64 rounds={a.rounds} mode={a.mode}: ms per step (stencil + sync), per-class wave stats in us")
+    print(f"n={n}^3 {a.dtype} rounds={a.rounds} mode={a.mode}: ms per step (stencil + sync), per-class wave stats in us")
     for v in (int(x) for x in a.variants.split(",")):
         pv = PLAIN_OF.get(v, v)
         tp = ev_time(lambda: native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], rd2, 1e-4,

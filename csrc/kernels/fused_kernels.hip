@@ -81,7 +81,8 @@ void fused_debug(int64_t* stamps, int force_sel) {
 }
 
 bool diffusion3d_fused_variant_ok(int v) {
-  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14 || v == 40 || v == 41 || v == 42 || v == 50;
+  return v == 0 || v == 2 || v == 9 || v == 11 || v == 14 || v == 40 || v == 41 || v == 42 || v == 44 || v == 45 ||
+         v == 50;
 }
 
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,

@@ -1,4 +1,4 @@
-// Fused halo-exchange diffusion kernels, fused variants 2 (v2_by4_ry4 prefetch), 9 (v4_by4_ry8), 14 (v4_bz2_by2_ry8).
+// Fused halo-exchange diffusion kernels, fused variants 2 (v2_by4_ry4 prefetch), 9 (v4_by4_ry8), 14 (v4_bz2_by2_ry8), 44 (14 + edge-lane z).
 // One translation unit per tiling family (igg/fused_impl.hpp) so they compile in parallel.
 #include "igg/fused_impl.hpp"
 
@@ -11,6 +11,9 @@ bool dispatch_misc(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode
     case 2: launch_mode<T, 4, 4, 2, true, 1>(d, io, mode, s); break;
     case 9: launch_mode<T, 4, 8, 4, false, 1>(d, io, mode, s); break;
     case 14: launch_mode<T, 2, 8, 4, false, 2>(d, io, mode, s); break;
+    // + edge-lane z exchange (FEAT 8192: no per-row v_readlane, which the
+    // one-wave-per-SIMD f32 form of tiling 14 cannot hide: profiles/r2_f32_fused/)
+    case 44: launch_mode<T, 2, 8, 4, false, 2, 8192>(d, io, mode, s); break;
     default: return false;
   }
   return true;

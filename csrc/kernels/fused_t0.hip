@@ -10,6 +10,7 @@ bool dispatch_t0(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, 
   switch (v) {
     case 0: launch_mode<T, 4, 4, 4, false, 1>(d, io, mode, s); break;
     case 50: launch_mode<T, 4, 4, 4, false, 1, 1024>(d, io, mode, s); break;  // tiling 0, one WG per CU
+    case 45: launch_mode<T, 4, 4, 4, false, 1, 8192>(d, io, mode, s); break;  // tiling 0 + edge-lane z
     default: return false;
   }
   return true;
