@@ -443,6 +443,9 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
         cands += FUSED_DIRECT
         if model.T.dtype.itemsize == 4:
             cands += FUSED_DIRECT_F32
+    # every form also with its exchanged x planes peeled off the chunk sweep
+    # (send mode bit 8: profiles/r2_peel/, -1.8 % f64 / -2.8 % f32 interior rank)
+    cands += [(v, fm | 8, gr) for v, fm, gr in cands]
     if os.environ.get("IGG_FUSED_CANDIDATES"):  # "v/mode/rounds,..." (measurements)
         cands = [tuple(int(x) for x in c.split("/")) for c in os.environ["IGG_FUSED_CANDIDATES"].split(",")]
     t_unf, times = float("inf"), {}

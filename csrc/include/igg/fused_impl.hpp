@@ -83,6 +83,7 @@ struct HxScal {
   // force_sel >= 0 runs every wave with that feature class.
   int64_t* stamps;
   int force_sel;
+  int peel;  // send mode bit 8: sweep the exchanged x planes of a chunk separately (kernel below)
 };
 
 
@@ -99,7 +100,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
          const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
          const T* __restrict__ yi1, const T* __restrict__ zi0, const T* __restrict__ zi1,
          T* __restrict__ xo0, T* __restrict__ xo1, T* __restrict__ yo0, T* __restrict__ yo1,
-         T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T>& a) {
+         T* __restrict__ zo0, T* __restrict__ zo1, const HxScal<T>& a, int64_t clip_lo = 0,
+         int64_t clip_hi = INT64_MAX) {
   using V = typename Vec<T, VZ>::type;
   constexpr int W = 64 * VZ * BZ;
   // FEAT 65536 (RV, plain sweeps only): reversed march - chunks from the top x
@@ -127,8 +129,10 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   const int64_t n0 = a.n0, n1 = a.n1, n2 = a.n2, s0 = n1 * n2;
   const int64_t zt = tz * W + wz * (64 * VZ);
   const int64_t y0 = 1 + ty * (BY * RY) + wy * RY;
-  const int64_t xs = 1 + cx * a.ch;
-  const int64_t xe = min(xs + a.ch, n0 - 1);
+  // [clip_lo, clip_hi): the part of the chunk this call sweeps (the kernel
+  // peels the exchanged x planes off a chunk: see diffusion3d_hx_kernel)
+  const int64_t xs = max<int64_t>(1 + cx * a.ch, clip_lo);
+  const int64_t xe = min(min<int64_t>(1 + cx * a.ch + a.ch, n0 - 1), clip_hi);
   const int nv = static_cast<int>(min<int64_t>(RY, n1 - 1 - y0));
   if (nv <= 0 || xs >= xe) return;
   const int64_t hi2 = n2 - 1;
@@ -480,6 +484,9 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
 #define IGG_HX_SWEEP(F)                                                                                  \
   hx_sweep<T, BY, RY, VZ, PF, BZ, DF, (F)>(t2, t, cpp, xi0, xi1, yi0, yi1, zi0, zi1, xo0, xo1, yo0, yo1, \
                                            zo0, zo1, a)
+#define IGG_HX_SWEEP_R(F)                                                                                \
+  hx_sweep<T, BY, RY, VZ, PF, BZ, DF, (F)>(t2, t, cpp, xi0, xi1, yi0, yi1, zi0, zi1, xo0, xo1, yo0, yo1, \
+                                           zo0, zo1, a, clo, chi)
   if constexpr ((FX | FY | FZ) == 0 || (FEAT & 2048) != 0) {
     IGG_HX_SWEEP(FEAT);  // nothing to specialise, or specialisation disabled (FEAT 2048)
   } else {
@@ -507,15 +514,36 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     int sel = __builtin_amdgcn_readfirstlane((wx ? 1 : 0) | (wyy ? 2 : 0) | (wzz ? 4 : 0));
     if (a.force_sel >= 0) sel = a.force_sel;
     const int64_t t_start = a.stamps ? wall_clock64() : 0;
-    switch (sel) {
-      case 0: IGG_HX_SWEEP(FK); break;
-      case 1: IGG_HX_SWEEP(FK | FX); break;
-      case 2: IGG_HX_SWEEP(FK | FY); break;
-      case 3: IGG_HX_SWEEP(FK | FX | FY); break;
-      case 4: IGG_HX_SWEEP(FK | FZ); break;
-      case 5: IGG_HX_SWEEP(FK | FX | FZ); break;
-      case 6: IGG_HX_SWEEP(FK | FY | FZ); break;
-      default: IGG_HX_SWEEP(FEAT); break;
+    // Peel (a.peel): an x-chunk wave needs the x exchange only at x = 1 (reads
+    // plane 0 from the arena, sends plane 1) and x = n0-2 (sends it, reads
+    // plane n0-1); the planes in between are swept with the x features
+    // compiled out (up to 3 parts; each part reloads its first 3 planes).
+    int64_t plo_[3], phi_[3];
+    int psel[3], np = 1;
+    plo_[0] = 0;
+    phi_[0] = INT64_MAX;
+    psel[0] = sel;
+    if (a.peel && (sel & 1) && a.force_sel < 0) {
+      const bool lo = xs == 1 && (xi0 || xo0), hi = xe == n0 - 1 && (xi1 || xo1);
+      int64_t a0 = xs;
+      np = 0;
+      if (lo) { plo_[np] = xs; phi_[np] = xs + 1; psel[np++] = sel; a0 = xs + 1; }
+      const int64_t b0 = hi ? n0 - 2 : xe;
+      if (b0 > a0) { plo_[np] = a0; phi_[np] = b0; psel[np++] = sel & ~1; }
+      if (hi && n0 - 2 >= a0) { plo_[np] = n0 - 2; phi_[np] = n0 - 1; psel[np++] = sel; }
+    }
+    for (int p = 0; p < np; ++p) {
+      const int64_t clo = plo_[p], chi = phi_[p];
+      switch (__builtin_amdgcn_readfirstlane(psel[p])) {
+        case 0: IGG_HX_SWEEP_R(FK); break;
+        case 1: IGG_HX_SWEEP_R(FK | FX); break;
+        case 2: IGG_HX_SWEEP_R(FK | FY); break;
+        case 3: IGG_HX_SWEEP_R(FK | FX | FY); break;
+        case 4: IGG_HX_SWEEP_R(FK | FZ); break;
+        case 5: IGG_HX_SWEEP_R(FK | FX | FZ); break;
+        case 6: IGG_HX_SWEEP_R(FK | FY | FZ); break;
+        default: IGG_HX_SWEEP_R(FEAT); break;
+      }
     }
     if (a.stamps) {
       // one vector store per wave (lane 0; lane-dependent address -> VGPR store)
@@ -530,6 +558,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     }
   }
 #undef IGG_HX_SWEEP
+#undef IGG_HX_SWEEP_R
 }
 
 int resident(const void* kernel, int block, size_t lds = 0) {
@@ -546,7 +575,7 @@ int resident(const void* kernel, int block, size_t lds = 0) {
 }
 
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
-void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream) {
+void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream, bool peel = false) {
   const int64_t n0 = d.n[0], n1 = d.n[1], n2 = d.n[2];
   if (n2 % VZ != 0 || n2 < 2 * VZ)
     fail("diffusion3d (fused halo): n2 must be a multiple of ", VZ, " and >= ", 2 * VZ);
@@ -574,6 +603,7 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
   a.dtlam = static_cast<T>(d.dt_lam);
   a.stamps = g_hx_stamps;
   a.force_sel = g_hx_force_sel;
+  a.peel = peel ? 1 : 0;
   auto in = [&](int k, int s) { return reinterpret_cast<const T*>(io.in[k][s]); };
   auto out = [&](int k, int s) { return reinterpret_cast<T*>(io.out[k][s]); };
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(block), lds, stream,
@@ -602,6 +632,10 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream)
 // field (one element per row, the row's own 64-B line) instead of a packed
 // arena region, so no wave patches a received z halo into its rows (the cost
 // of the z-edge waves of tilings 11/40: profiles/r2_fused_spec/).
+//
+// Mode bit 8 (peel): a wave of an x-exchange chunk sweeps x = 1 and x = n0-2
+// with the x features and the planes in between without them (the x code in
+// the loop slows the whole chunk's march: profiles/r2_f32_fused/ class 1).
 // XF: extra FEAT bits of the tiling (512 | 1024 for fused variant 40).
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, int XF = 0>
 void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStream_t s) {
@@ -613,21 +647,23 @@ void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStre
     }
   }
   const bool zx = io.in[2][0] || io.in[2][1] || io.out[2][0] || io.out[2][1];
+  const bool pk = (mode & 8) != 0;  // peel the exchanged x planes (kernel)
+  mode &= 7;
   if ((mode & 4) && zx) {
     // Direct z (FEAT 203 = 207 without z-in): the z sends land in the
     // receivers' field halo elements, so the z-edge waves read their halo
     // from the field like every other wave and carry only the send code.
     if (io.in[2][0] || io.in[2][1]) fail("diffusion3d (fused halo): direct z mode with z arena input");
-    if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF>(d, io, s);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF>(d, io, s);
+    if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF>(d, io, s, pk);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF>(d, io, s, pk);
   } else if (zx || !(mode & 2)) {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s, pk);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s, pk);
   } else {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF>(d, io, s);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF>(d, io, s);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF>(d, io, s, pk);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF>(d, io, s, pk);
   }
 }
 

@@ -140,9 +140,11 @@ class Diffusion3D:
         # Fused kernel: variant (tiling; one with a fused instantiation) and
         # send mode (0 stores as computed, 1 deferred one x step; +2 compiles the
         # z-edge exchange out when there is no z neighbour; +4 direct z: the z
-        # faces go straight into the neighbours' next T, no z receive code).
+        # faces go straight into the neighbours' next T, no z receive code; +8
+        # peel: x-chunk waves sweep only x = 1 / n0-2 with the x exchange,
+        # profiles/r2_peel/).
         self.fused_variant = 0
-        self.fused_mode = 0
+        self.fused_mode = 8
         self.fused_rounds = 3  # grid residency rounds (profiles/r1_fused/grid.log)
         self._fh = None
         self._fstep = 0
@@ -176,7 +178,7 @@ class Diffusion3D:
                 except Exception as e:  # collective outcome: every rank gets here together
                     warnings.warn(f"Diffusion3D: direct z sends unavailable ({e})")
             if self.fused_mode & 4 and not self._fh.has_fields:
-                self.fused_mode &= 3
+                self.fused_mode &= ~4
             if not stencil.native.diffusion3d_fused_variant_ok(int(self.fused_variant)):
                 self.fused_variant = 0
             self.set_overlap(False)

@@ -116,6 +116,26 @@ def test_fused_direct_z_matches_update_halo(gpu, variant, dtype, mode, periods):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [8, 9, 12, 13])
+@pytest.mark.parametrize("variant", [0, 14, 40, 42, 44])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("periods", [(1, 1, 1), (1, 0, 1)])
+def test_fused_peel_matches_update_halo(gpu, variant, dtype, mode, periods):
+    """Mode bit 8 (peel): x-chunk waves sweep x = 1 / n0-2 with the x exchange
+    and the planes between without it (multi-plane chunks on this grid, so
+    first, middle and last parts all run); same results as update_halo_."""
+    a, b = _pair((48, 130, 264), periods, dtype, variant, mode=mode)
+    assert b.fused_mode == mode
+    a.run(7)
+    b.run(7)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
 def test_fused_direct_z_graph(gpu):
     """Direct z under hipGraph replays (both buffer parities captured) and the
     loopback emulation's remote path."""
