@@ -331,11 +331,13 @@ constexpr Variant VARIANTS[] = {
     {"hx_v2_by4_ry8_nt_zl_occ1", 4, 8, 2, false, true}, // 40 (one workgroup per CU)
     {"hx_v2_by4_ry10_nt_zl_occ1", 4, 10, 2, false, true}, // 41
     {"hx_v2_by4_ry12_nt_zl_occ1", 4, 12, 2, false, true}, // 42
+    // 43: full-row z tiles (BZ 4 x 64 lanes x VZ 2 = 512 points, profiles/r2_fullrow/)
+    {"hx_v2_bz4_by2_ry8_nt", 2, 8, 2, false, true},     // 43
 };
 // Variants 21..31: restrict-form tiling id (fused_kernels.hip dispatch_plain)
 // and the stencil_kernels.hip variant used for boxes other than the inner box.
-constexpr int HX_TILING[] = {0, 2, 9, 11, 14, 100, 101, 102, 103, 104, 105, 110, 111, 112, 113, 120, 121, 122, 123, 124, 125, 126};
-constexpr int HX_FALLBACK[] = {0, 2, 9, 11, 14, 11, 11, 11, 2, 5, 11, 11, 0, 9, 14, 11, 9, 11, 0, 11, 11, 11};
+constexpr int HX_TILING[] = {0, 2, 9, 11, 14, 100, 101, 102, 103, 104, 105, 110, 111, 112, 113, 120, 121, 122, 123, 124, 125, 126, 141};
+constexpr int HX_FALLBACK[] = {0, 2, 9, 11, 14, 11, 11, 11, 2, 5, 11, 11, 0, 9, 14, 11, 9, 11, 0, 11, 11, 11, 11};
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
 // Grid sizing policy: `g_rounds` full residency rounds (resident workgroups =

@@ -58,8 +58,9 @@ def _variant_for(T, boxes, rd2, dtlam, T2, Cp, stream) -> int:
 # Variants that win somewhere on MI355X (sweeps in profiles/): v4_by4_ry4_nt,
 # v2_by4_ry4_pf_nt, v4_by4_ry4, v4_by4_ry8_nt, v2_by4_ry8_nt, v4_bz2_by2_ry8_nt.
 # 21+: restrict-argument (fused-kernel) form; 40: lane-distributed z-segment edge
-# loads at one workgroup per CU (profiles/r1_zl/).
-SHORTLIST = (0, 2, 9, 11, 14, 21, 23, 24, 25, 26, 40)
+# loads at one workgroup per CU (profiles/r1_zl/); 43: full-row z tiles
+# (profiles/r2_fullrow/).
+SHORTLIST = (0, 2, 9, 11, 14, 21, 23, 24, 25, 26, 40, 43)
 # Grid residency rounds tried per variant by the model autotune: 1-4 measured
 # best depending on the box and variant (profiles/r1_fused/grid.log,
 # variant_sweep.log, r1_zl/: 1-2.5 %).
