@@ -147,7 +147,8 @@ def self_launch(args) -> int:
             # queues oversubscribe the device's queue slots and the command
             # processor time-slices them (8 ranks: 7.9 ms/step vs 0.25 with one
             # queue per process, profiles/r2_reh8/). One rank per GPU never does.
-            env.setdefault("GPU_MAX_HW_QUEUES", "1")
+            # Overrides the environment's value (the GPU boxes export 4).
+            env["GPU_MAX_HW_QUEUES"] = "1"
         out = tempfile.TemporaryFile(mode="w+")
         outs.append(out)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
