@@ -694,6 +694,7 @@ def main():
                 "warmup_steps_run": args.warmup + extra,
                 "loopback_emulation": bool(args.loopback),
                 "self_launched": os.environ.get("IGG_BENCH_SELF_LAUNCHED") == "1",
+                "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "hip_graph": getattr(model, "graph", None) is not None,
                 "hip_graph_error": graph_error,
                 "timing_bracket": ("rccl all-reduce + stream event + synchronize" if _BRACKET["dev"] and nprocs > 1

@@ -34,6 +34,18 @@ def test_self_launch_reports_n_gpus(n):
     assert rec["ms_per_step"] == rec["config"]["t_it_ms"]
 
 
+def test_share_gpu_self_launch_forces_one_hw_queue():
+    """--share-gpu with > 2 ranks runs every rank with one hardware queue, even
+    when the environment exports more (the GPU boxes export 4: N x 4 queues on
+    one device are time-sliced, profiles/r2_reh8/)."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--share-gpu", "--device", "cpu", "--n", "20",
+                        "--steps", "2", "--warmup", "1"], capture_output=True, text=True, timeout=150,
+                       env=_env(GPU_MAX_HW_QUEUES="4"), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["n_gpus"] == 3 and rec["config"]["hw_queues"] == "1"
+
+
 def test_world_size_mismatch_is_an_error():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--n", "16", "--steps", "1",
                         "--warmup", "0"], capture_output=True, text=True, timeout=60,
