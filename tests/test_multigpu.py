@@ -94,7 +94,10 @@ def test_diffusion_8_ranks_matches_global(transport):
                                                # the halo column of the neighbour's next field
                                                (2, (24, 20, 64, 6, 1, 0), ("40", "4")),
                                                (8, (18, 20, 136, 5, 0, 1), ("42", "4")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("0", "5"))])
+                                               (8, (16, 18, 24, 6, 1, 1), ("0", "5")),
+                                               # peeled x planes (mode bit 8)
+                                               (2, (40, 66, 136, 6, 1, 0), ("42", "12")),
+                                               (8, (34, 66, 136, 5, 1, 1), ("40", "8"))])
 def test_fused_exchange_across_devices(nprocs, cfg, kernel):
     """Stencil kernel stores its send planes into the neighbours' arenas over
     xGMI: bitwise equal to stencil + update_halo_ (RCCL) on every rank."""
