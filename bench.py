@@ -74,6 +74,15 @@ FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4))
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
+# What "value" is, appended to every metric label (BASELINE.json names the
+# metric per GPU; the bench contract asks for the whole-job aggregate).
+VALUE_LABEL = (" [value: whole-job aggregate GB/s = sum of the per-GPU T_eff over n_gpus GPUs; "
+               "per GPU: config.t_eff_per_gpu_GBs]")
+# Bitwise checks of the fused exchange against the update_halo_ path: a quick
+# filter before the A/B, a long one for the candidate that is kept, and one
+# after the timed region (from the state the timed steps left).
+FUSED_CHECK_STEPS = 24
+FUSED_KEEP_CHECK_STEPS = 200
 # BASELINE.json configs. The driver runs the default (the headline metric).
 CONFIGS = {
     "diffusion3d": dict(model="diffusion3d", n=512, dtype="float64", gather_every=0, metric=METRIC),
@@ -348,6 +357,57 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
     return out
 
 
+def post_validate(field, comm, log, on_gpu: bool) -> dict:
+    """After the timed region: one update_halo_ of the probe payload through
+    the transport and schedule the timed steps used, compared bitwise with the
+    host-staged gloo exchange (the reference's non-GPU-aware path). Collective;
+    every rank agrees. The transport / schedule settings are restored.
+    (CPU plumbing runs have one path only: the comparison is with itself.)"""
+    import torch
+
+    from igg.parallel import halo as H
+
+    X0 = _probe_field(field)
+    if on_gpu:
+        t, gmode = H.transport_name(), H.halo_mode()
+        sched = "put" if t == "put" else H.plan_mode(field)
+    else:
+        t, gmode, sched = "host", None, "sequential"
+    why = ""
+    try:
+        if on_gpu and t != "put":
+            H.set_halo_mode(sched)
+        X = X0.clone()
+        H.update_halo_(X)
+        if on_gpu:
+            _sync(comm)
+        H.check_transport()
+        if on_gpu:
+            H.set_transport("staged")
+            H.set_halo_mode("sequential")
+        R = X0.clone()
+        H.update_halo_(R)
+        if on_gpu:
+            _sync(comm)
+        if _inject("post_validation"):
+            X.view(-1)[X.numel() // 2] += 1
+        if not torch.equal(X, R):
+            bad = (X != R).nonzero()
+            why = f"mismatch at {bad.shape[0]} entries, first {bad[0].tolist()}"
+    except Exception as e:  # a bounded wait expired, a transport error
+        why = f"{type(e).__name__}: {e}"[:300]
+        if getattr(comm, "mesh", None) is not None:
+            comm.mesh.clear_error()
+    finally:
+        if on_gpu:
+            H.set_transport(t)
+            H.set_halo_mode(gmode)
+    fails = _max_over_ranks(comm, 1.0 if why else 0.0)
+    res = "ok" if fails == 0.0 else (why or "failed on another rank")
+    log(f"post-timing validation {t}/{sched} vs staged: {res}")
+    return {"transport": t, "schedule": sched, "result": res}
+
+
 def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, dict]:
     """A/B timing of the validated transports / schedules on the model's step
     (graph replays, MAX over ranks); keeps the fastest."""
@@ -384,7 +444,15 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
     return best, {k: round(v[0] * 1e3, 5) for k, v in times.items()}
 
 
-def _fused_check(model, comm, log, nchk: int = 24) -> bool:
+def _inject(what: str) -> bool:
+    """Test hook (IGG_BENCH_INJECT=what[,what]): corrupt one element on rank 0
+    of the named check's result, to prove the check fails closed."""
+    from igg.parallel.grid import global_grid
+
+    return what in os.environ.get("IGG_BENCH_INJECT", "").split(",") and int(global_grid().me) == 0
+
+
+def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = "") -> bool:
     """Bitwise check of the model's CURRENT fused kernel (variant / send mode /
     grid rounds) against the update_halo_ path: ``nchk`` steps from the same
     state on every rank, in the timed run's execution shape (a primed arena,
@@ -408,6 +476,8 @@ def _fused_check(model, comm, log, nchk: int = 24) -> bool:
         model.sync_halo()
         _sync(comm)
         model.check()
+        if inject and _inject(inject):
+            model.T.view(-1)[model.T.numel() // 2] += 1
         ok = bool(torch.equal(ref, model.T))
     except Exception as e:  # e.g. a sync kernel timed out: this fused kernel does not work here
         log(f"fused check v{model.fused_variant}/m{model.fused_mode}/r{model.fused_rounds} failed: "
@@ -434,7 +504,6 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
     if not _fused_check(model, comm, log):
         log("fused halo exchange mismatched the update_halo_ path on some rank: excluded")
         return {"fused_ok": False}
-    checked = {(model.fused_variant, model.fused_mode, model.fused_rounds)}
     # Fused kernel candidates: tiling variant x send mode (0 = stores as
     # computed, 1 = deferred one x step: robust to slow remote acknowledgements).
     # Two interleaved passes of 20 steps, best of the two per candidate: the
@@ -466,7 +535,8 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
         if not (mode == "on" or t_fus < t_unf):
             break
         model.fused_variant, model.fused_mode, model.fused_rounds = cand
-        if cand in checked or _fused_check(model, comm, log):
+        # the kept candidate: a long check whatever the quick one said
+        if _fused_check(model, comm, log, nchk=FUSED_KEEP_CHECK_STEPS):
             keep, best = True, cand
             break
         rejected.append(name(cand))
@@ -478,7 +548,8 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
         + ", ".join(f"fused {name(k)}={t * 1e3:.4f}" for k, t in times.items())
         + f" -> {'fused ' + name(best) if keep else 'update_halo'}"
         + (f" (failed their bitwise check: {', '.join(rejected)})" if rejected else ""))
-    out = {"fused_ok": True, "update_halo": round(t_unf * 1e3, 5)}
+    out = {"fused_ok": True, "update_halo": round(t_unf * 1e3, 5),
+           "kept_check_steps": FUSED_KEEP_CHECK_STEPS if keep else None}
     out.update({f"fused_{name(k)}": round(t * 1e3, 5) for k, t in times.items()})
     if rejected:
         out["fused_rejected"] = rejected
@@ -587,36 +658,93 @@ def main():
         k = max(1, getattr(model, "graph_steps", 1) if getattr(model, "graph", None) is not None else 1)
         extra = int(-(-warm_ms // (est * k))) * k
         model.run(extra)
-    sync()
-    _bracket(comm)
-    t0 = time.perf_counter()
-    if gather_every > 0:
-        done, pending = 0, None
-        snap = torch.empty_like(field()) if args.gather_mode == "async" and on_gpu else None
-        while done < args.steps:
-            k = min(gather_every, args.steps - done)
-            model.run(k)
-            done += k
-            if done % gather_every == 0:
-                if getattr(model, "fused", False):
-                    model.sync_halo()  # fused steps leave the halo planes stale
-                if snap is None:
-                    igg.gather_(field(), A_global)
-                else:
-                    if pending is not None:
-                        pending.wait()
-                    snap.copy_(field())
-                    pending = igg.gather_async_(snap, A_global)
-        if pending is not None:
-            pending.wait()
-    else:
-        model.run(args.steps)
-    _bracket(comm)
-    t1 = time.perf_counter()
-    elapsed = _max_over_ranks(comm, t1 - t0)
+    def timed_region() -> float:
+        """The timed region: exactly ``args.steps`` full steps (plus the
+        configured gathers) between two barrier+synchronize brackets; MAX over
+        ranks of the wall time."""
+        sync()
+        _bracket(comm)
+        t0 = time.perf_counter()
+        if gather_every > 0:
+            done, pending = 0, None
+            snap = torch.empty_like(field()) if args.gather_mode == "async" and on_gpu else None
+            while done < args.steps:
+                k = min(gather_every, args.steps - done)
+                model.run(k)
+                done += k
+                if done % gather_every == 0:
+                    if getattr(model, "fused", False):
+                        model.sync_halo()  # fused steps leave the halo planes stale
+                    if snap is None:
+                        igg.gather_(field(), A_global)
+                    else:
+                        if pending is not None:
+                            pending.wait()
+                        snap.copy_(field())
+                        pending = igg.gather_async_(snap, A_global)
+            if pending is not None:
+                pending.wait()
+        else:
+            model.run(args.steps)
+        _bracket(comm)
+        t1 = time.perf_counter()
+        return _max_over_ranks(comm, t1 - t0)
+
+    elapsed = timed_region()
     H.check_transport()
     if hasattr(model, "check"):
         model.check()
+    # After the timed region: prove the steps that were timed computed the
+    # right field, and fail closed if not (a wrong field never yields a number).
+    #  1. fused exchange: K fused vs K update_halo_ steps from the state the
+    #     timed steps left, bitwise; on a mismatch the fused exchange is
+    #     dropped and the region re-timed on the update_halo_ path;
+    #  2. every multi-rank run: the probe payload through the transport and
+    #     schedule the timed steps used, bitwise vs the host-staged reference;
+    #     on a mismatch the run is re-timed on the next validated schedule, and
+    #     fails (no JSON line) when none is left.
+    fused_post = None
+    if getattr(model, "fused", False):
+        n_post = max(args.steps, FUSED_KEEP_CHECK_STEPS)
+        ok = _fused_check(model, comm, log, nchk=n_post, inject="fused_post")
+        fused_post = {"steps": n_post, "result": "ok" if ok else "mismatch"}
+        if ok:
+            model.set_fused(True)
+        else:
+            log("fused halo exchange: post-timing check FAILED; re-timing on the update_halo_ path")
+            fused_post["fallback"] = "update_halo_ (re-timed)"
+            model.graph = None
+            if graph_ok:
+                model.capture()
+            model.run(extra)  # the same untimed warm load as before the first region
+            elapsed = timed_region()
+            H.check_transport()
+    post_valid = None
+    if nprocs > 1:
+        post_valid = post_validate(field(), comm, log, on_gpu)
+        tried = [(post_valid["transport"], post_valid["schedule"])]
+        while post_valid["result"] != "ok":
+            nxt = next(((t, m) for name, t, m in TRANSPORT_CANDIDATES
+                        if (valid or {}).get(name) == "ok" and (t, m) not in tried), None)
+            if nxt is None:
+                log(f"bench: post-timing validation failed ({post_valid['result']}) and no validated schedule "
+                    f"is left: no result")
+                raise SystemExit(1)
+            log(f"bench: post-timing validation of {tried[-1]} failed: re-timing with {nxt}")
+            tried.append(nxt)
+            if getattr(model, "fused", False):
+                model.set_fused(False)
+            H.set_transport(nxt[0])
+            H.set_halo_mode(nxt[1])
+            model.graph = None
+            if graph_ok:
+                model.capture()
+            model.run(extra)
+            elapsed = timed_region()
+            H.check_transport()
+            failed = post_valid
+            post_valid = post_validate(field(), comm, log, on_gpu)
+            post_valid["replaced"] = failed
     t_it = elapsed / args.steps
     per_gpu = model.a_eff_bytes / t_it / 1e9
     total = per_gpu * nprocs
@@ -645,9 +773,9 @@ def main():
         gather_ms = round(_max_over_ranks(comm, time.perf_counter() - tg) * 1e3, 3)
     if me == 0:
         out = {
-            "metric": cfg["metric"],
+            "metric": cfg["metric"] + VALUE_LABEL,
             "value": round(total, 3),
-            "unit": "GB/s",
+            "unit": "GB/s (aggregate over n_gpus)",
             "n_gpus": nprocs,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -682,6 +810,8 @@ def main():
                 if nprocs > 1 or args.loopback else None,
                 "halo_mode_measured": H.tuned_modes() or None,
                 "validation": valid,
+                "post_validation": post_valid,
+                "fused_post_check": fused_post,
                 "transport_ab_ms": ab,
                 "fused_halo": bool(getattr(model, "fused", False)),
                 "fused_kernel": ({"variant": model.fused_variant, "mode": model.fused_mode,

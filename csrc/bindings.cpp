@@ -33,6 +33,68 @@ using namespace igg;
 
 namespace {
 
+// DLPack (v0.8 ABI, the layout torch.utils.dlpack consumes): a native device
+// allocation of a given memory kind handed to torch as a 1-D uint8 tensor
+// whose deleter frees it. Lets a model keep its fields in fine-grained memory
+// (docs/COHERENCE.md) without linking libtorch.
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+constexpr int32_t kDLROCM = 10;
+
+struct DlpackAlloc {
+  int64_t shape[1];
+  int device;
+};
+
+void dlpack_free(DLManagedTensor* t) {
+  if (!t) return;
+  auto* ctx = static_cast<DlpackAlloc*>(t->manager_ctx);
+  int cur = 0;
+  if (hipGetDevice(&cur) == hipSuccess && cur != ctx->device) (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();  // no kernel may still use the buffer
+  (void)hipFree(t->dl_tensor.data);
+  if (cur != ctx->device) (void)hipSetDevice(cur);
+  delete ctx;
+  delete t;
+}
+
+py::capsule alloc_dlpack(size_t bytes, int kind) {
+  if (bytes == 0) fail("alloc_dlpack: zero bytes");
+  int dev = 0;
+  IGG_HIP_CHECK(hipGetDevice(&dev));
+  void* p = ipc_malloc(bytes, static_cast<MemKind>(kind));
+  auto* ctx = new DlpackAlloc{{static_cast<int64_t>(bytes)}, dev};
+  auto* t = new DLManagedTensor{};
+  t->dl_tensor.data = p;
+  t->dl_tensor.device = {kDLROCM, dev};
+  t->dl_tensor.ndim = 1;
+  t->dl_tensor.dtype = {1 /* kDLUInt */, 8, 1};
+  t->dl_tensor.shape = ctx->shape;
+  t->dl_tensor.strides = nullptr;
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = ctx;
+  t->deleter = dlpack_free;
+  // Unconsumed capsules free their tensor; torch renames a consumed one to
+  // "used_dltensor" and owns the deleter from then on.
+  return py::capsule(t, "dltensor", [](PyObject* cap) {
+    if (PyCapsule_IsValid(cap, "dltensor")) dlpack_free(static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor")));
+  });
+}
+
 hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 using FieldTuple = std::tuple<uintptr_t, int, std::array<int64_t, 3>, std::array<int64_t, 3>, int, bool>;
@@ -192,6 +254,8 @@ PYBIND11_MODULE(_igg_native, m) {
     return reinterpret_cast<uintptr_t>(ipc_malloc(bytes, static_cast<MemKind>(kind)));
   });
   m.def("ipc_free", [](uintptr_t p) { ipc_free(reinterpret_cast<void*>(p)); });
+  m.def("alloc_dlpack", &alloc_dlpack, py::arg("bytes"), py::arg("kind"),
+        "Zeroed device allocation of a MemKind as a DLPack capsule (1-D uint8; torch.utils.dlpack.from_dlpack).");
   m.def("ipc_get_handle", [](uintptr_t p) { return py::bytes(ipc_get_handle(reinterpret_cast<void*>(p))); });
   m.def("ipc_open", [](const std::string& h) { return reinterpret_cast<uintptr_t>(ipc_open(h)); });
   m.def("ipc_close", [](uintptr_t p) { ipc_close(reinterpret_cast<void*>(p)); });
@@ -337,6 +401,18 @@ PYBIND11_MODULE(_igg_native, m) {
            }),
            py::arg("uid"), py::arg("nranks"), py::arg("rank"))
       .def("barrier", [](RcclComm& c, uintptr_t s) { c.barrier(as_stream(s)); })
+      .def("allreduce",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t s) {
+             c.allreduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count, dtype, op,
+                         as_stream(s));
+           },
+           py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"), py::arg("op"), py::arg("stream"))
+      .def("broadcast",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int root, uintptr_t s) {
+             c.broadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count, dtype, root,
+                         as_stream(s));
+           },
+           py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"), py::arg("root"), py::arg("stream"))
       .def("check_async_error", &RcclComm::check_async_error)
       .def("abort", &RcclComm::abort)
       .def_property_readonly("rank", &RcclComm::rank)

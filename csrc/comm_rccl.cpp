@@ -84,6 +84,51 @@ void RcclComm::barrier(hipStream_t stream) {
   IGG_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, stream));
 }
 
+namespace {
+
+ncclDataType_t nccl_type(int d) {
+  switch (d) {
+    case RcclComm::I8: return ncclInt8;
+    case RcclComm::U8: return ncclUint8;
+    case RcclComm::I32: return ncclInt32;
+    case RcclComm::U32: return ncclUint32;
+    case RcclComm::I64: return ncclInt64;
+    case RcclComm::U64: return ncclUint64;
+    case RcclComm::F16: return ncclFloat16;
+    case RcclComm::F32: return ncclFloat32;
+    case RcclComm::F64: return ncclFloat64;
+    case RcclComm::BF16: return ncclBfloat16;
+    default: fail("RcclComm: unsupported dtype code ", d);
+  }
+  return ncclUint8;
+}
+
+ncclRedOp_t nccl_op(int op) {
+  switch (op) {
+    case 0: return ncclSum;
+    case 1: return ncclProd;
+    case 2: return ncclMax;
+    case 3: return ncclMin;
+    default: fail("RcclComm: unsupported reduction op ", op);
+  }
+  return ncclSum;
+}
+
+}  // namespace
+
+void RcclComm::allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream) {
+  if (aborted_) fail("RCCL communicator was aborted");
+  if (count == 0) return;
+  IGG_NCCL_CHECK(ncclAllReduce(send, recv, count, nccl_type(dtype), nccl_op(op), comm_, stream));
+}
+
+void RcclComm::broadcast(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t stream) {
+  if (aborted_) fail("RCCL communicator was aborted");
+  if (root < 0 || root >= nranks_) fail("RcclComm.broadcast: root ", root, " out of range");
+  if (count == 0) return;
+  IGG_NCCL_CHECK(ncclBroadcast(send, recv, count, nccl_type(dtype), root, comm_, stream));
+}
+
 void RcclComm::check_async_error() {
   if (aborted_) fail("RCCL communicator was aborted after a communication failure");
   ncclResult_t st = ncclSuccess;

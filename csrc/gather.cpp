@@ -78,13 +78,16 @@ PullGatherer::PullGatherer(int rank, int nranks, AllGather allgather)
     : rank_(rank), nranks_(nranks), allgather_(std::move(allgather)) {
   peer_key_.assign(nranks, std::string());
   peer_ev_.assign(nranks, nullptr);
+  mapped_.assign(nranks, {std::string(), nullptr});
 }
 
 PullGatherer::~PullGatherer() {
   for (hipStream_t s : side_) (void)hipStreamSynchronize(s);
-  for (auto& o : opened_) (void)hipIpcCloseMemHandle(o.second);
-  opened_.clear();
+  for (auto& m : mapped_)
+    if (m.second) (void)hipIpcCloseMemHandle(m.second);
   for (hipEvent_t& e : peer_ev_)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : root_done_)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : done_) (void)hipEventDestroy(e);
   if (ready_) (void)hipEventDestroy(ready_);
@@ -98,7 +101,7 @@ void PullGatherer::ensure_streams() {
     hipStream_t s;
     hipEvent_t e;
     IGG_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    IGG_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    IGG_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventInterprocess | hipEventDisableTiming));
     side_.push_back(s);
     done_.push_back(e);
   }
@@ -107,8 +110,10 @@ void PullGatherer::ensure_streams() {
 void PullGatherer::free() {
   if (pending_) fail("gather_async: free while a gather is pending (call wait() first)");
   for (hipStream_t s : side_) IGG_HIP_CHECK(hipStreamSynchronize(s));
-  for (auto& o : opened_) (void)hipIpcCloseMemHandle(o.second);
-  opened_.clear();
+  for (auto& m : mapped_) {
+    if (m.second) (void)hipIpcCloseMemHandle(m.second);
+    m = {std::string(), nullptr};
+  }
 }
 
 void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream) {
@@ -116,14 +121,16 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
   if (pending_) fail("gather_async: a gather is already pending (call wait() first)");
   if (!a.device) fail("gather_async: the local array must be a GPU array.");
   if (dims[0] * dims[1] * dims[2] != nranks_) fail("gather_async: dims do not match the number of processes.");
+  if (root < 0 || root >= nranks_) fail("gather_async: root ", root, " out of range");
   if (rank_ == root && !dst) fail("The input argument A_global can't be `nothing` on the root");
   ensure_streams();
-  // `a` is final where the caller's stream has got to now: an interprocess
-  // event marks that point (the root's copies wait on it; no host drain).
+  const size_t EH = sizeof(hipIpcEventHandle_t), MH = sizeof(hipIpcMemHandle_t);
+  // `a` (and, on the root, dst) is final where the caller's stream has got to
+  // now: an interprocess event marks that point (no host drain).
   IGG_HIP_CHECK(hipEventRecord(ready_, stream));
   hipIpcEventHandle_t eh;
   IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, ready_));
-  std::string mine(reinterpret_cast<const char*>(&eh), sizeof(eh));
+  std::string mine(reinterpret_cast<const char*>(&eh), EH);
   if (rank_ != root) {
     void* base = nullptr;
     size_t size = 0;
@@ -131,22 +138,29 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
     hipIpcMemHandle_t h;
     IGG_HIP_CHECK(hipIpcGetMemHandle(&h, base));
     const uint64_t off = a.ptr - reinterpret_cast<uintptr_t>(base);
-    mine.append(reinterpret_cast<const char*>(&h), sizeof(h));
+    mine.append(reinterpret_cast<const char*>(&h), MH);
     mine.append(reinterpret_cast<const char*>(&off), sizeof(off));
+  } else {
+    for (hipEvent_t e : done_) {  // the peers order their streams after these in wait()
+      IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, e));
+      mine.append(reinterpret_cast<const char*>(&eh), EH);
+    }
   }
   // Host rendezvous only (every rank has recorded its event before the root
   // waits on it), not a GPU drain.
   const std::vector<std::string> all = allgather_(mine);
-  used_ = 0;
+  if (static_cast<int>(all.size()) != nranks_) fail("gather_async: allgather returned ", all.size(), " entries");
+  const int nside = static_cast<int>(side_.size());
+  used_ = std::min(nranks_, nside);
   if (rank_ == root) {
-    const size_t EH = sizeof(hipIpcEventHandle_t), MH = sizeof(hipIpcMemHandle_t);
-    const int nside = static_cast<int>(side_.size());
+    // Every copy stream starts behind the root's own stream: its earlier work
+    // on dst (a fill, a previous consumer of a reused allocation) comes first.
+    for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipStreamWaitEvent(side_[k], ready_, 0));
     for (int p = 0; p < nranks_; ++p) {
       const Int3 c{p / (dims[1] * dims[2]), (p / dims[2]) % dims[1], p % dims[2]};
       hipStream_t s = side_[p % nside];
       const void* src = nullptr;
       if (p == root) {
-        IGG_HIP_CHECK(hipStreamWaitEvent(s, ready_, 0));
         src = reinterpret_cast<const void*>(a.ptr);
       } else {
         const std::string& rec = all[p];
@@ -162,15 +176,37 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
         IGG_HIP_CHECK(hipStreamWaitEvent(s, peer_ev_[p], 0));
         uint64_t off = 0;
         std::memcpy(&off, rec.data() + EH + MH, 8);
-        // Mapped for this gather only: the peer may free its array after wait().
-        void* base = ipc_open(rec.substr(EH, MH));
-        opened_.emplace_back(rec.substr(EH, MH), base);
-        src = static_cast<const char*>(base) + off;
+        const std::string mkey = rec.substr(EH, MH);
+        auto& m = mapped_[p];
+        if (m.first != mkey) {  // this rank's array lives in another allocation now
+          if (m.second) {
+            for (hipStream_t q : side_) IGG_HIP_CHECK(hipStreamSynchronize(q));  // rare: old copies drained
+            ipc_close(m.second);
+          }
+          m = {mkey, ipc_open(mkey)};
+        }
+        src = static_cast<const char*>(m.second) + off;
       }
       copy_block(src, dst, a.size, dims, c, a.elem_bytes, s);
     }
-    used_ = std::min(nranks_, nside);
     for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipEventRecord(done_[k], side_[k]));
+  } else {
+    const std::string& rec = all[root];
+    if (rec.size() != EH * (1 + used_)) fail("gather_async: malformed handles from the root");
+    if (static_cast<int>(root_done_.size()) < used_) {
+      root_done_.resize(used_, nullptr);
+      root_key_.resize(used_);
+    }
+    for (int k = 0; k < used_; ++k) {
+      const std::string key = rec.substr(EH * (1 + k), EH);
+      if (root_key_[k] != key) {
+        if (root_done_[k]) IGG_HIP_CHECK(hipEventDestroy(root_done_[k]));
+        hipIpcEventHandle_t h;
+        std::memcpy(&h, key.data(), EH);
+        IGG_HIP_CHECK(hipIpcOpenEventHandle(&root_done_[k], h));
+        root_key_[k] = key;
+      }
+    }
   }
   root_ = root;
   pending_ = true;
@@ -179,15 +215,13 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
 void PullGatherer::wait(hipStream_t stream) {
   TraceRange tr("igg.gather_async.wait");
   if (!pending_) fail("gather_async: no pending gather");
-  if (rank_ == root_) {
-    for (int k = 0; k < used_; ++k) {
-      IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_[k], 0));  // later work on A_global
-      IGG_HIP_CHECK(hipEventSynchronize(done_[k]));             // pulls done: peers may reuse their arrays
-    }
-    for (auto& o : opened_) ipc_close(o.second);
-    opened_.clear();
-  }
+  if (rank_ == root_)
+    for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipStreamWaitEvent(stream, done_[k], 0));  // later work on dst
+  // The root recorded its done events in start(), before this rendezvous: from
+  // here on every rank's waits refer to this gather's records.
   (void)allgather_(std::string());
+  if (rank_ != root_)
+    for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipStreamWaitEvent(stream, root_done_[k], 0));  // later writes to `a`
   pending_ = false;
 }
 

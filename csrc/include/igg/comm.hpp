@@ -62,6 +62,13 @@ class RcclComm : public Transport {
 
   // Device-side barrier: 1-element all-reduce on `stream` (caller syncs).
   void barrier(hipStream_t stream);
+  // Collectives on raw device buffers, enqueued on `stream` (comm_cart interop:
+  // the applications' MPI.Allreduce!/MPI.Bcast! on the grid communicator,
+  // README.md:166-178 of the reference). dtype: DType codes below; op:
+  // 0 sum, 1 prod, 2 max, 3 min. In place when send == recv.
+  enum DType : int { I8 = 0, U8 = 1, I32 = 2, U32 = 3, I64 = 4, U64 = 5, F16 = 6, F32 = 7, F64 = 8, BF16 = 9 };
+  void allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream);
+  void broadcast(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t stream);
   // Raises igg::Error if the communicator reported an asynchronous failure.
   void check_async_error();
   void abort();

@@ -50,9 +50,10 @@ struct ParityShift {
 };
 
 // Device: enqueue all copies (any count, split in MAX_BATCH chunks) on `stream`.
-// system_fence: every thread ends by waiting for its stores to be acknowledged
-// (put transport: stores into a peer's uncached arena are performed before the
-// following sync kernel publishes them).
+// system_fence: every wave ends by waiting for its stores and writing its
+// XCD's L2 back at system scope (put transport: stores into a peer's
+// fine-grained arena reach the owner before the following sync kernel
+// publishes them; docs/COHERENCE.md).
 void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
                    bool system_fence = false, const ParityShift& parity = ParityShift{});
 

@@ -7,8 +7,10 @@
 // a fused step is two launches on one stream:
 //   1. the stencil (launch_diffusion3d_fused): while sweeping the interior it
 //      stores the planes each neighbour needs (x=1/n0-2, y=1/n1-2, z=1/n2-2)
-//      into that neighbour's IPC-mapped, uncached arena, and reads its own
-//      face halos from its arena instead of from the field;
+//      into that neighbour's IPC-mapped, fine-grained arena, and reads its
+//      own face halos from its arena instead of from the field; every wave
+//      that stored to a peer ends with a system-scope release (wave_release
+//      in fused_impl.hpp);
 //   2. the put-transport sync kernel (1 wave): publish "my step arrived" at
 //      every neighbour, wait for theirs (bounded spins, error flag on timeout).
 // The arena has two halves: step i writes half i&1 and reads half (i-1)&1, so
@@ -18,11 +20,15 @@
 // materialises them when a caller needs them (gather, output, mode switch).
 // Direct z (mode bit 4, set_fields): the z faces skip the arena and land in
 // the halo column of the neighbour's next field, which the neighbour's next
-// step reads like any other element. Safe for the same reason as the arena:
-// a neighbour writes my buffer k (halo elements only) during the step in
-// which my stencil writes buffer k's interior and reads buffer 1-k; my
-// previous step (which read buffer k) finished before that neighbour's sync
-// kernel let it start this step.
+// step reads like any other element. Ordering: a neighbour writes my buffer k
+// (halo elements only) during the step in which my stencil writes buffer k's
+// interior and reads buffer 1-k; my previous step (which read buffer k)
+// finished before that neighbour's sync kernel let it start this step.
+// Coherence: the halo element shares a cache line with interior elements my
+// own kernel is writing at the same time, from another device. HIP defines
+// that for fine-grained memory only, so across devices the fields must be
+// fine-grained (Diffusion3D's default field_memory="fine"). docs/COHERENCE.md
+// has the whole argument.
 // Results are bitwise identical to stencil + update_halo_ (tests/test_fused.py).
 #pragma once
 

@@ -86,6 +86,38 @@ struct HxScal {
   int peel;  // send mode bit 8: sweep the exchanged x planes of a chunk separately (kernel below)
 };
 
+// Writer side of the cross-device hand-off (docs/COHERENCE.md): every store
+// into peer memory (arena regions, or the neighbour's field with direct z) is
+// a system-scope store (sc0 sc1 = the encoding of a relaxed system-scope
+// atomic store on gfx942/gfx950): it writes through this XCD's L2, where the
+// peer mapping (MTYPE NC) could otherwise keep it dirty, and its vmcnt
+// acknowledgement means it reached the owner's memory. The wave ends with
+// s_waitcnt vmcnt(0) (hx_sweep), so when this kernel completes every peer
+// byte has landed; the sync kernel then publishes the flag. (A plain store +
+// per-wave buffer_wbl2 sc0 sc1 also works but writes back the XCD's whole
+// L2 from every storing wave: +14 % per step, profiles/r3_coherence/.)
+// Inline asm without a memory clobber: the destinations never alias anything
+// this kernel reads (restrict arguments), so the compiler may keep
+// scheduling loads across them; untracked by its vmcnt bookkeeping, the
+// stores only make its waits more conservative (in-order vmcnt on gfx9).
+template <typename V>
+__device__ __forceinline__ void st_sys(V* p, const V& v) {
+  static_assert(sizeof(V) == 4 || sizeof(V) == 8 || sizeof(V) == 16 || sizeof(V) == 32, "st_sys: 4..32 B");
+  if constexpr (sizeof(V) == 32) {
+    using H = unsigned __attribute__((ext_vector_type(4)));
+    struct P2 { H lo, hi; };
+    const P2 h = __builtin_bit_cast(P2, v);
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(h.lo));
+    asm volatile("global_store_dwordx4 %0, %1, off offset:16 sc0 sc1" ::"v"(p), "v"(h.hi));
+  } else if constexpr (sizeof(V) == 16) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+  } else if constexpr (sizeof(V) == 8) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+  } else {
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+  }
+}
+
 
 // FEAT bits (compile-time exchange features): 1 x-in, 2 y-in, 4 z-in, 8 z-out,
 // 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants); 512 =
@@ -338,8 +370,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
       }
     }
     if constexpr (DF) {
-      if (ysend_dst) *reinterpret_cast<V*>(ysend_dst) = ysend;
-      if (zsend_dst) *zsend_dst = zv;
+      if (ysend_dst) st_sys(reinterpret_cast<V*>(ysend_dst), ysend);
+      if (zsend_dst) st_sys(zsend_dst, zv);
       ysend_dst = nullptr;
       zsend_dst = nullptr;
     }
@@ -396,16 +428,16 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         }
         // Send planes / rows (whole vectors of the lanes that own them: the
         // halo elements they carry are never read by the receiver).
-        if (xd0 && zown) *reinterpret_cast<V*>(xd0 + rowb[r] + zl) = out;
-        if (xd1 && zown) *reinterpret_cast<V*>(xd1 + rowb[r] + zl) = out;
+        if (xd0 && zown) st_sys(reinterpret_cast<V*>(xd0 + rowb[r] + zl), out);
+        if (xd1 && zown) st_sys(reinterpret_cast<V*>(xd1 + rowb[r] + zl), out);
         if (r == 0 && yrow0) {
           if (DF) { ysend = out; ysend_dst = zown ? yrow0 + x * n2 + zl : nullptr; }
-          else if (zown) *reinterpret_cast<V*>(yrow0 + x * n2 + zl) = out;
+          else if (zown) st_sys(reinterpret_cast<V*>(yrow0 + x * n2 + zl), out);
         }
         if (r == ry1) {
           // one deferral slot: taken by row 0 if this wave also sends that row
           if (DF && !yrow0) { ysend = out; ysend_dst = zown ? yrow1 + x * n2 + zl : nullptr; }
-          else if (zown) *reinterpret_cast<V*>(yrow1 + x * n2 + zl) = out;
+          else if (zown) st_sys(reinterpret_cast<V*>(yrow1 + x * n2 + zl), out);
         }
         if constexpr (ZE && (FEAT & 8) != 0) {
           zo_buf[r] = has_lo ? out[1] : out[VZ - 2];  // the send element of the edge lane
@@ -434,7 +466,7 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     }
     if (zdst) {
       if (DF) zsend_dst = zdst + x * a.zp;
-      else zdst[x * a.zp] = zv;
+      else st_sys(zdst + x * a.zp, zv);
     }
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
@@ -455,11 +487,12 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     }
   }
   if constexpr (DF) {  // sends of the last step
-    if (ysend_dst) *reinterpret_cast<V*>(ysend_dst) = ysend;
-    if (zsend_dst) *zsend_dst = zv;
+    if (ysend_dst) st_sys(reinterpret_cast<V*>(ysend_dst), ysend);
+    if (zsend_dst) st_sys(zsend_dst, zv);
   }
-  // Remote stores acknowledged before the wave retires (the sync kernel that
-  // publishes the arrival flags runs after this kernel on the same stream).
+  // Remote stores (system scope, st_sys) acknowledged before the wave retires:
+  // the sync kernel that publishes the arrival flags runs after this kernel
+  // on the same stream.
   if (remote) __builtin_amdgcn_s_waitcnt(0);
 }
 

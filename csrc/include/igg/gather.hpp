@@ -45,19 +45,25 @@ class Gatherer {
 // Non-blocking gather by root pull (MI355X copy engines), stream-ordered.
 // start(): every rank records an interprocess event on its own stream where
 // `a` is final (no host-side drain of the GPU) and publishes that event's IPC
-// handle plus the IPC handle + offset of the allocation holding `a`; the root
-// makes its copy streams wait on every rank's event and enqueues, per block,
-// ONE 3-D copy from the (peer-mapped) block straight into its place in
-// `dst` (hipMemcpy3DAsync: rows of s2 elements at the global pitch; a P2P copy
-// over xGMI for peer blocks). No staging buffer and no reorder pass: the
-// global array is written once. Blocks are spread over up to 8 copy streams so
-// the transfers from different peers (different xGMI links) run concurrently.
-// start() returns immediately: the application keeps computing while the
-// data moves. wait(): the root orders the caller's stream after the copies and
-// waits for them; every rank then passes a barrier, after which the peers may
-// modify `a` again (MPI_Igather semantics: `a` is read-only until wait()
-// returns). Peer memory mappings live from start() to wait(); peer events are
-// opened once and cached.
+// handle plus the IPC handle + offset of the allocation holding `a` (the root
+// publishes the handles of its per-copy-stream "done" events instead); the
+// root makes every copy stream it uses wait on its own event first (earlier
+// work of its stream on `dst`, e.g. a zero fill, stays ahead of every copy),
+// then on the event of the rank whose block it pulls, and enqueues ONE 3-D copy
+// per block from the (peer-mapped) block straight into its place in `dst`
+// (hipMemcpy3DAsync: rows of s2 elements at the global pitch; a P2P copy over
+// xGMI for peer blocks), then records its done events. No staging buffer and
+// no reorder pass: the global array is written once. Blocks are spread over up
+// to 8 copy streams so the transfers from different peers (different xGMI
+// links) run concurrently. start() returns immediately: the application keeps
+// computing while the data moves.
+// wait(): nothing blocks on the GPU. The root orders its stream after its done
+// events; a host rendezvous (the done events of this gather are recorded before
+// it) lets every other rank order ITS stream after the root's done events
+// (opened once through IPC), so its later work on `a` (MPI_Igather semantics:
+// `a` is read-only until then) queues behind the pulls on the device.
+// Peer mappings are cached per rank and closed when that rank's allocation
+// changes (after the copy streams drained) or at free().
 class PullGatherer {
  public:
   using AllGather = std::function<std::vector<std::string>(const std::string&)>;
@@ -77,14 +83,16 @@ class PullGatherer {
   int rank_, nranks_;
   AllGather allgather_;
   std::vector<hipStream_t> side_;  // copy streams (root)
-  std::vector<hipEvent_t> done_;   // one per copy stream
+  std::vector<hipEvent_t> done_;   // one per copy stream (interprocess)
   hipEvent_t ready_ = nullptr;     // interprocess: `a` final on the caller's stream
   std::vector<std::string> peer_key_;  // IPC event handle bytes per rank (cache key)
   std::vector<hipEvent_t> peer_ev_;    // opened peer events (root)
+  std::vector<std::string> root_key_;  // non-root: the root's done-event handles (cache keys)
+  std::vector<hipEvent_t> root_done_;  // non-root: the root's done events, opened
+  std::vector<std::pair<std::string, void*>> mapped_;  // root: per rank (handle, base) of `a`'s allocation
   bool pending_ = false;
   int root_ = 0;
   int used_ = 0;  // copy streams used by the pending gather
-  std::vector<std::pair<std::string, void*>> opened_;  // peer mappings of the pending gather
 };
 
 }  // namespace igg

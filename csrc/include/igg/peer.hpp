@@ -10,9 +10,14 @@
 // field shapes, so sender and receiver agree without negotiation; the two
 // halves let exchange e+1's puts land while e is still being unpacked.
 //
-// Arenas and flags are uncached device memory (coherent across devices: remote
-// stores land in HBM without passing through any L2, local reads bypass L2, so
-// the only release needed is "stores acknowledged"), exported once with
+// Memory kinds (the full ordering / coherence argument: docs/COHERENCE.md):
+// flag words are uncached (hipDeviceMallocUncached: every access goes to
+// memory, polls see a peer's store without any cache maintenance); arenas are
+// fine-grained (hipDeviceMallocFinegrained: HIP defines concurrent access by
+// other devices while a kernel runs). A writer's stores into a peer arena may
+// sit dirty in the writer's XCD L2 (the peer mapping is MTYPE NC there), so
+// every storing wave ends with a system-scope release (buffer_wbl2 sc0 sc1)
+// before the sync kernel publishes its flag. Both are exported once with
 // hipIpcGetMemHandle and re-exported (collectively) only when an arena grows.
 #pragma once
 
@@ -73,9 +78,8 @@ class PeerMesh {
   std::vector<void*> mapped_;  // map_buffers() mappings (one per distinct peer allocation)
   void unmap_buffers();
   int64_t timeout_ticks_ = 0;
-  // Fine-grained (coherent across devices; reads cached in L2 within a kernel,
-  // invalidated at kernel-boundary acquires): the fused stencil's halo reads
-  // from the arena cost 6 us/step instead of 12 with the uncached kind
+  // Fine-grained: the fused stencil's halo reads from the arena cost 6 us/step
+  // instead of 12 with the uncached kind, whose reads bypass the L2
   // (profiles/r2_arena/; IGG_PUT_ARENA_KIND=3 restores uncached).
   MemKind arena_kind_ = MemKind::FineGrained;
   hipStream_t side_ = nullptr;

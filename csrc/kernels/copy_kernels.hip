@@ -21,12 +21,31 @@ constexpr int64_t CHUNK = BLOCK * EPT;         // elements of a row per workgrou
 struct alignas(16) B16 { uint64_t x, y; };
 
 // Byte shift of the arena half selected by the device-resident epoch (odd ->
-// second half). The epoch lives in uncached memory written by the put
-// transport's begin kernel earlier on the same stream.
+// second half). The epoch lives in the uncached flag words, written by the
+// put transport's sync kernel earlier on the same stream.
 __device__ __forceinline__ int64_t parity_shift(const CopyBatch& b) {
   if (b.parity_side == 0) return 0;
   const uint64_t e = __hip_atomic_load(b.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return ((e + b.parity_add) & 1) ? b.parity_bytes : 0;
+}
+
+// Element store: plain, or (SYS, put transport) a system-scope store
+// (sc0 sc1, the encoding of a relaxed system-scope atomic store on gfx950).
+template <typename T, bool SYS>
+__device__ __forceinline__ void store(T* p, const T& v) {
+  if constexpr (!SYS) {
+    *p = v;
+  } else if constexpr (sizeof(T) == 16) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v)));
+  } else if constexpr (sizeof(T) == 8) {
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+  } else if constexpr (sizeof(T) == 4) {
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+  } else if constexpr (sizeof(T) == 2) {
+    asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p), "v"(static_cast<unsigned>(v)));
+  } else {
+    asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p), "v"(static_cast<unsigned>(v)));
+  }
 }
 
 template <typename T, bool FENCE>
@@ -46,8 +65,8 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
     const int64_t e = local * BLOCK + threadIdx.x;
     if (e < cp.n_outer * cp.n_inner) {
       const int64_t o = e / cp.n_inner, i = e - o * cp.n_inner;
-      reinterpret_cast<T*>(dbase)[o * cp.dst_so + i * cp.dst_si] =
-          reinterpret_cast<const T*>(sbase)[o * cp.src_so + i * cp.src_si];
+      store<T, FENCE>(reinterpret_cast<T*>(dbase) + o * cp.dst_so + i * cp.dst_si,
+                      reinterpret_cast<const T*>(sbase)[o * cp.src_so + i * cp.src_si]);
     }
   } else {
     const int64_t nchunks = (cp.n_inner + CHUNK - 1) / CHUNK;
@@ -65,26 +84,15 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int64_t i = i0 + k * BLOCK + threadIdx.x;
-      if (i < n) dst[i * cp.dst_si] = v[k];
+      if (i < n) store<T, FENCE>(dst + i * cp.dst_si, v[k]);
     }
   }
-  // Put transport, cross-device ordering argument (writer side):
-  //  1. the destination arena is IPC-mapped peer memory allocated uncached
-  //     (MemKind::Uncached: MTYPE UC), so these stores bypass this GPU's L2
-  //     and travel over xGMI to the owner's HBM; there is no dirty line to
-  //     write back at any scope;
-  //  2. s_waitcnt vmcnt(0) below holds the wave until every one of its stores
-  //     has been acknowledged by the memory system that owns the address
-  //     (for a remote address: after the write reached the peer's fabric /
-  //     memory controller). A workgroup-scope release fence would NOT wait
-  //     for this on gfx9 outside tgsplit mode, hence the explicit wait;
-  //  3. the sync kernel runs after this kernel on the same in-order stream
-  //     (AQL barrier bit: it starts only once every wave here retired), issues
-  //     __threadfence_system() and only then stores the ARRIVED flag into the
-  //     receiver's flag words with a system-scope release;
-  //  4. the receiver's sync kernel observes the flag with a system-scope
-  //     acquire load; its unpack kernel reads the (uncached) arena after that
-  //     kernel on the same stream, so it cannot see pre-put data.
+  // Put transport (FENCE): every store above was a system-scope store into a
+  // peer's fine-grained arena (written through this XCD's L2, where the peer
+  // mapping could keep a plain store dirty); the wave waits for their
+  // acknowledgements before it retires, then the sync kernel that runs next
+  // on this stream publishes the ARRIVED flag and the receiver reads the
+  // arena only after observing it (docs/COHERENCE.md).
   if (FENCE) __builtin_amdgcn_s_waitcnt(0);
 }
 

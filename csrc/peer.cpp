@@ -133,22 +133,34 @@ std::vector<std::vector<char*>> PeerMesh::map_buffers(const std::vector<uintptr_
     (void)allgather_(std::string());
     unmap_buffers();
   }
-  // Record per buffer: handle of its allocation + offset inside it.
+  // Record per buffer: handle of its allocation + offset inside it, behind a
+  // one-byte status. A rank that cannot export its buffers still joins the
+  // allgather (status 0) so every rank fails together instead of the others
+  // blocking in the collective.
   const size_t hb = sizeof(hipIpcMemHandle_t);
-  std::string rec;
-  if (nranks_ > 1)
-    for (uintptr_t p : mine) {
-      void* base = nullptr;
-      size_t size = 0;
-      IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(p)));
-      const uint64_t off = p - reinterpret_cast<uintptr_t>(base);
-      rec += ipc_get_handle(base);
-      rec.append(reinterpret_cast<const char*>(&off), 8);
-    }
-  const std::vector<std::string> all = allgather_(rec);
+  std::string rec(1, '1'), error;
+  try {
+    if (nranks_ > 1)
+      for (uintptr_t p : mine) {
+        void* base = nullptr;
+        size_t size = 0;
+        IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(p)));
+        const uint64_t off = p - reinterpret_cast<uintptr_t>(base);
+        rec += ipc_get_handle(base);
+        rec.append(reinterpret_cast<const char*>(&off), 8);
+      }
+  } catch (const Error& e) {
+    error = e.what();
+    rec.assign(1, '0');
+  }
+  std::vector<std::string> all = allgather_(rec);
   if (static_cast<int>(all.size()) != nranks_) fail("PeerMesh: allgather returned ", all.size(), " entries");
+  for (int r = 0; r < nranks_; ++r)
+    if (all[r].empty() || all[r][0] != '1')
+      fail("PeerMesh: rank ", r, " could not export its buffers",
+           error.empty() ? std::string() : std::string(" (here: ") + error + ")");
+  for (auto& a : all) a.erase(0, 1);
   std::vector<std::vector<char*>> out(nranks_);
-  std::string error;
   try {
     for (int r = 0; r < nranks_; ++r) {
       if (r == rank_) {

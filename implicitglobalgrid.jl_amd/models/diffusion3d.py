@@ -66,7 +66,7 @@ class Diffusion3D:
     def __init__(self, *, dtype=torch.float64, device=None, lam: float = 1.0, cp_min: float = 1.0,
                  lx: float = 10.0, ly: float = 10.0, lz: float = 10.0, overlap: bool = False,
                  slab_width=None, variant=None, halo_variant=None, interior_rounds: int = 0,
-                 halo_rounds: int = 0, reserve_cus: int = 0):
+                 halo_rounds: int = 0, reserve_cus: int = 0, field_memory: str = None):
         gg = _grid.global_grid()
         nx, ny, nz = (int(v) for v in gg.nxyz)
         if device is None:
@@ -105,8 +105,20 @@ class Diffusion3D:
         # One allocation with gaps between the three arrays: measured 1-3 %
         # faster than back-to-back 2 MiB-aligned tensors on MI355X
         # (benchmarks/stencil_offsets.py: HBM channel placement).
+        # field_memory (IGG_FIELD_MEMORY): "fine" (default: one native
+        # fine-grained allocation) or "torch" (coarse-grained, torch's caching
+        # allocator). The direct-z fused exchange stores into the neighbours'
+        # T/T2 while their kernels run, which HIP defines for fine-grained
+        # memory only (docs/COHERENCE.md); the plain sweep runs as fast on it
+        # (profiles/r3_coherence/: 0.6222 vs 0.6263 ms/step).
+        import os as _os
+
+        self.field_memory = (field_memory or _os.environ.get("IGG_FIELD_MEMORY", "fine")).strip().lower()
+        if self.field_memory not in ("torch", "fine"):
+            raise ValueError(f"Diffusion3D: field_memory must be 'torch' or 'fine', got {self.field_memory!r}")
         if self.device.type == "cuda":
-            self.T, self.Cp, self.T2 = _carve([self.T, self.Cp, self.T2], gap=266240)
+            self.T, self.Cp, self.T2 = _carve([self.T, self.Cp, self.T2], gap=266240,
+                                              kind=1 if self.field_memory == "fine" else None)
         sides = [[bool(gg.neighbors[0, d] != -1), bool(gg.neighbors[1, d] != -1)] for d in range(3)]
         self.sides = sides
         self.can_overlap = self.device.type == "cuda" and any(any(sd) for sd in sides)
@@ -173,10 +185,14 @@ class Diffusion3D:
         if flag:
             if self._fh is None:
                 self._fh = _make_fused_halo(self)
-                try:  # direct z sends (fused_mode bit 4) write into the neighbours' T/T2
-                    self._fh.set_fields(self.T.data_ptr(), self.T2.data_ptr())
-                except Exception as e:  # collective outcome: every rank gets here together
-                    warnings.warn(f"Diffusion3D: direct z sends unavailable ({e})")
+                # Direct z sends (fused_mode bit 4) write into the neighbours'
+                # T/T2 while their kernels run: defined for fine-grained fields
+                # (docs/COHERENCE.md); torch-allocated fields only on one GPU.
+                if self.field_memory == "fine" or _grid.global_grid().nprocs == 1:
+                    try:
+                        self._fh.set_fields(self.T.data_ptr(), self.T2.data_ptr())
+                    except Exception as e:  # collective outcome: every rank gets here together
+                        warnings.warn(f"Diffusion3D: direct z sends unavailable ({e})")
             if self.fused_mode & 4 and not self._fh.has_fields:
                 self.fused_mode &= ~4
             if not stencil.native.diffusion3d_fused_variant_ok(int(self.fused_variant)):
@@ -391,17 +407,33 @@ def _make_fused_halo(m: "Diffusion3D"):
     return native.FusedHalo(mesh, list(m.T.shape), m.T.element_size(), nb)
 
 
-def _carve(tensors, gap: int):
-    """Copies of equally sized tensors placed in one buffer ``gap`` bytes apart."""
+def _carve(tensors, gap: int, kind=None):
+    """Copies of equally sized tensors placed in one buffer ``gap`` bytes apart.
+    ``kind``: None = torch's caching allocator, else a native MemKind (1 =
+    fine-grained) allocated by the runtime and handed over through DLPack."""
     nbytes = tensors[0].numel() * tensors[0].element_size()
     stride = nbytes + gap
-    buf = torch.empty(stride * len(tensors), dtype=torch.uint8, device=tensors[0].device)
+    if kind is None:
+        buf = torch.empty(stride * len(tensors), dtype=torch.uint8, device=tensors[0].device)
+    else:
+        buf = native_buffer(stride * len(tensors), kind, tensors[0].device)
     out = []
     for k, t in enumerate(tensors):
         v = buf[k * stride:k * stride + nbytes].view(t.dtype).view(t.shape)
         v.copy_(t)
         out.append(v)
     return out
+
+
+def native_buffer(nbytes: int, kind: int, device) -> torch.Tensor:
+    """1-D uint8 device tensor of ``nbytes`` in native memory of MemKind
+    ``kind`` (csrc/include/igg/ipc.hpp), owned by torch (freed with it)."""
+    from torch.utils import dlpack
+
+    from .._native import native
+
+    with torch.cuda.device(device):
+        return dlpack.from_dlpack(native.alloc_dlpack(int(nbytes), int(kind)))
 
 
 def _choose_variant(m: "Diffusion3D") -> int:

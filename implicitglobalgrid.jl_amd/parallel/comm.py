@@ -163,15 +163,23 @@ class Communicator:
     # -- tensor collectives (comm_cart interop) --------------------------------
     # The reference hands applications its MPI Cartesian communicator for their
     # own collectives (README.md:166-178: e.g. a global residual). Here: CPU
-    # tensors over gloo, GPU tensors over RCCL (torch's nccl backend) ordered on
-    # the caller's current stream.
+    # tensors over gloo, GPU tensors over the grid's own native RCCL
+    # communicator (the one that carries the halo traffic: one RCCL
+    # communicator per rank), ordered on the caller's current stream.
     _OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "prod": "PRODUCT"}
+    _RCCL_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+    _RCCL_TYPES = {torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4, torch.float16: 6,
+                   torch.float32: 7, torch.float64: 8, torch.bfloat16: 9}
 
-    def _tensor_group(self, t: torch.Tensor):
-        if not t.is_cuda:
-            return self.gloo
-        self._ensure_torch_nccl()
-        return self.torch_nccl
+    def _rccl_tensor(self, t: torch.Tensor):
+        """(rccl communicator, dtype code, count) for a GPU tensor; complex
+        tensors travel as their real pairs."""
+        if not t.is_contiguous():
+            raise IGGError("comm collectives on GPU tensors need a contiguous tensor")
+        v = torch.view_as_real(t) if t.is_complex() else t
+        if v.dtype not in self._RCCL_TYPES:
+            raise IGGError(f"comm collectives: unsupported GPU dtype {t.dtype}")
+        return self.ensure_rccl(), self._RCCL_TYPES[v.dtype], v.numel()
 
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         """In-place all-reduce of ``t`` over the grid's ranks (``op``: sum,
@@ -179,7 +187,14 @@ class Communicator:
         if op not in self._OPS:
             raise IGGError(f"allreduce_: op must be one of {sorted(self._OPS)} (got {op!r})")
         if self.size > 1:
-            dist.all_reduce(t, op=getattr(dist.ReduceOp, self._OPS[op]), group=self._tensor_group(t))
+            if t.is_cuda:
+                if t.is_complex() and op != "sum":
+                    raise IGGError(f"allreduce_: op {op!r} is not defined for complex tensors")
+                rc, dt, n = self._rccl_tensor(t)
+                rc.allreduce(t.data_ptr(), t.data_ptr(), n, dt, self._RCCL_OPS[op],
+                             torch.cuda.current_stream().cuda_stream)
+            else:
+                dist.all_reduce(t, op=getattr(dist.ReduceOp, self._OPS[op]), group=self.gloo)
         return t
 
     def bcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
@@ -188,7 +203,11 @@ class Communicator:
         if not 0 <= root < self.size:
             raise IGGError(f"bcast_: root {root} out of range 0..{self.size - 1}")
         if self.size > 1:
-            dist.broadcast(t, src=self.global_rank(root), group=self._tensor_group(t))
+            if t.is_cuda:
+                rc, dt, n = self._rccl_tensor(t)
+                rc.broadcast(t.data_ptr(), t.data_ptr(), n, dt, root, torch.cuda.current_stream().cuda_stream)
+            else:
+                dist.broadcast(t, src=self.global_rank(root), group=self.gloo)
         return t
 
     def allreduce(self, value: float, op: str = "sum") -> float:

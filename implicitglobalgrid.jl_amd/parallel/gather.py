@@ -7,9 +7,16 @@ the process with Cartesian coords (cx,cy,cz) lands at
 gathered into a 3-D ``A_global``); ``A_global`` may be ``None`` off-root; the
 root keeps a grow-only internal buffer until ``finalize_global_grid``.
 
-MI355X path: GPU ``A`` -> one RCCL group of receives on the root straight into
-a grow-only device buffer + a HIP reorder kernel (csrc/gather.cpp). CPU ``A``
--> gloo point-to-point into a grow-only host buffer + one strided reorder copy.
+MI355X paths (csrc/gather.cpp):
+* GPU ``A``, all ranks on one node (the default; IGG_GATHER_PULL=0 disables):
+  the root's copy engines pull every block over xGMI straight into its place
+  in ``A_global`` (one 3-D peer copy per block, up to 8 concurrent copy
+  streams, ordered by interprocess events): no staging buffer of
+  nprocs*|A| on the root and no reorder pass. Stream-ordered, no host drain.
+* GPU ``A`` otherwise: one RCCL group of receives on the root into a grow-only
+  device buffer + a HIP reorder kernel.
+* CPU ``A``: gloo point-to-point into a grow-only host buffer + one strided
+  reorder copy.
 """
 from __future__ import annotations
 
@@ -24,10 +31,11 @@ from .halo import field_tuple
 _host_buf = None  # grow-only flat uint8 host buffer
 _gatherer = None  # native device gatherer (grow-only device buffer)
 _puller = None  # native PullGatherer (gather_async_)
+_sync_puller = None  # native PullGatherer of the synchronous gather_ (pull path)
 
 
 def free_gather_buffer() -> None:
-    global _host_buf, _gatherer, _puller
+    global _host_buf, _gatherer, _puller, _sync_puller
     _host_buf = None
     if _gatherer is not None:
         _gatherer.free()
@@ -37,6 +45,16 @@ def free_gather_buffer() -> None:
             raise IGGError("free_gather_buffer: a gather_async_ is still pending (call wait() first).")
         _puller.free()
     _puller = None
+    if _sync_puller is not None:
+        _sync_puller.free()
+    _sync_puller = None
+
+
+def _pull_ok(gg) -> bool:
+    """Pull path for GPU fields: every rank on this node (IPC-mappable peers).
+    The same answer on every rank (the choice is collective)."""
+    c = gg.comm
+    return int(gg.nprocs) > 1 and c is not None and c.local_size == c.size and config.gather_pull()
 
 
 def _padded_shape(A: torch.Tensor) -> list[int]:
@@ -65,6 +83,9 @@ def gather_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) ->
         if A_global.dtype != A.dtype:
             raise IGGError("The input arguments A and A_global must have the same element type.")
     s = _padded_shape(A)
+    if A.is_cuda and gg.amdgpu_enabled and _pull_ok(gg):
+        _gather_pull(A, A_global, root, s, dims, me, nprocs, c)
+        return
     if A.is_cuda and nprocs > 1 and c.rccl is None and gg.amdgpu_enabled and config.transport_choice() == "rccl":
         c.ensure_rccl()
     if A.is_cuda and (nprocs == 1 or c.rccl is not None):
@@ -88,6 +109,25 @@ def _gather_device(A, A_global, root, s, dims, me, nprocs, c) -> None:
         if _gatherer is None:
             _gatherer = native.Gatherer()
         _gatherer.gather(field_tuple(A), dst.data_ptr() if dst is not None else 0, root, dims, c.rccl, stream)
+    if me == root and dst is not A_global:
+        A_global.copy_(dst)
+
+
+def _gather_pull(A, A_global, root, s, dims, me, nprocs, c) -> None:
+    """Synchronous gather_ through the pull path: start + wait of a native
+    PullGatherer (stream-ordered on the current stream of every rank)."""
+    global _sync_puller
+    A = A.contiguous()
+    dst = None
+    if me == root:
+        dst = A_global if (A_global.is_cuda and A_global.is_contiguous()) else torch.empty(
+            A_global.shape, dtype=A.dtype, device=A.device)
+        _global_view(dst, s, dims)  # validates the shape
+    if _sync_puller is None:
+        _sync_puller = native.PullGatherer(me, nprocs, lambda b: c.all_gather_object(bytes(b)))
+    stream = torch.cuda.current_stream().cuda_stream
+    _sync_puller.start(field_tuple(A), dst.data_ptr() if dst is not None else 0, root, dims, stream)
+    _sync_puller.wait(stream)
     if me == root and dst is not A_global:
         A_global.copy_(dst)
 

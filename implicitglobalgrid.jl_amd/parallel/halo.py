@@ -24,6 +24,13 @@ from . import grid as _grid
 _engine = None
 _plans: dict = {}
 _MAX_PLANS = 512
+# 'auto' schedule winners by a rank-invariant field-set signature (shapes,
+# strides, dtypes, device kind): every rank makes the same update_halo_ calls
+# on the same local shapes, so whether a call runs the (collective) tuning
+# never depends on per-rank allocator state such as data pointers or plan-cache
+# evictions (a rank that tuned alone would pair its extra exchanges with the
+# other ranks' normal ones).
+_sig_modes: dict = {}
 _buf_dtype = {False: None, True: None}
 _debug_sync = False
 _graphs: list = []  # weakrefs to hipGraphs that captured update_halo_
@@ -118,6 +125,7 @@ def set_halo_mode(mode: str) -> None:
     algorithm), 'onephase' (faces+edges+corners in one phase) or 'auto'."""
     _grid.check_initialized()
     _engine.set_mode(HALO_MODES[mode])
+    _sig_modes.clear()
     for p in _plans.values():
         p[3] = None  # an explicit mode wins; 'auto' measures again
 
@@ -149,6 +157,7 @@ def pack_mode(dim: int) -> str:
 def _init_engine(gg) -> None:
     global _engine, _debug_sync
     _plans.clear()
+    _sig_modes.clear()
     _engine = native.HaloEngine(_grid_info(gg))
     _engine.set_mode(HALO_MODES[config.halo_mode()])
     for d, m in enumerate(config.pack_modes()):
@@ -173,6 +182,7 @@ def _drop_engine() -> None:
     global _engine, _loopback_comm
     _release_graphs()
     _plans.clear()
+    _sig_modes.clear()
     if _engine is not None:
         _engine.pool_free()
     _engine = None
@@ -189,6 +199,7 @@ def set_transport(name: str) -> None:
     if not gg.amdgpu_enabled:
         raise IGGError("set_transport: the grid was not initialised for GPU fields")
     _engine.set_transport(gg.comm.device_transport(name), True)
+    _sig_modes.clear()
     for p in _plans.values():
         p[3] = None  # schedule costs differ per transport: 'auto' measures again
 
@@ -236,6 +247,7 @@ def engine():
 def sync_grid() -> None:
     """Push the (possibly test-mutated) grid topology into the native engine."""
     _plans.clear()
+    _sig_modes.clear()
     _engine.set_grid(_grid_info(_grid.global_grid()))
 
 
@@ -272,6 +284,7 @@ def enable_loopback(dims=(True, True, True)) -> None:
     _engine.set_grid(native.GridInfo(1, 2, gg.nxyz.tolist(), gg.overlaps.tolist(), nb, peers))
     _engine.set_transport(_loopback_comm, True)
     _plans.clear()
+    _sig_modes.clear()
 
 
 # --- argument checks (update_halo.jl:804-834) ---------------------------------
@@ -429,9 +442,11 @@ def update_halo_(*fields) -> None:
     fs, device, dtype, mode = p
     stream = torch.cuda.current_stream().cuda_stream if device else 0
     if mode is None and device and _engine.mode == HALO_MODES["auto"]:
-        if _remote_peers() and _engine.transport_name(True) != "put" \
+        sig = tuple((tuple(A.shape), tuple(A.stride()), A.dtype) for A in fields)
+        mode = p[3] = _sig_modes.get(sig)
+        if mode is None and _remote_peers() and _engine.transport_name(True) != "put" \
                 and not torch.cuda.is_current_stream_capturing():
-            mode = p[3] = _tune_mode(fs, stream)
+            mode = p[3] = _sig_modes[sig] = _tune_mode(fs, stream)
     _engine.exchange_set(fs, stream, -1 if mode is None or _engine.mode != HALO_MODES["auto"] else mode)
     _buf_dtype[device] = dtype
     if _debug_sync and device and not torch.cuda.is_current_stream_capturing():

@@ -111,3 +111,11 @@ def comm_timeout(env: Mapping[str, str] | None = None) -> float:
     rank raises (default 300)."""
     env = os.environ if env is None else env
     return float(env.get("IGG_COMM_TIMEOUT", "300"))
+
+
+def gather_pull(env: Mapping[str, str] | None = None) -> bool:
+    """IGG_GATHER_PULL (default 1): GPU ``gather_`` on a single node pulls every
+    block with the root's copy engines straight into ``A_global`` (no staging
+    buffer of nprocs*|A|, no reorder pass); 0 = RCCL receives + reorder kernel."""
+    env = os.environ if env is None else env
+    return env.get("IGG_GATHER_PULL", "1").strip() not in ("0", "false", "no")

@@ -220,19 +220,24 @@ def scenario_gather_async():
             final = (torch.full(s, float(me + 1), dtype=torch.float64) * 1000
                      + torch.arange(120, dtype=torch.float64).view(s)).to(dt).cuda()
             A = torch.zeros(s, dtype=dt, device="cuda")
-            G = torch.zeros(dims[0] * 6, dims[1] * 5, dims[2] * 4, dtype=dt, device="cuda") if me == root else None
-            torch.cuda.synchronize()
-            # A becomes final only behind a long kernel on this rank's stream and
-            # gather_async_ is called without a host sync: the root's pull must
-            # be ordered after that point (interprocess events), not before.
+            G = torch.empty(dims[0] * 6, dims[1] * 5, dims[2] * 4, dtype=dt, device="cuda") if me == root else None
+            # No host sync anywhere below. A becomes final only behind a long
+            # kernel on every rank's stream (the root's is longer), and the
+            # root zero-fills G behind it: the root's pulls must be ordered
+            # after its own stream's fill (every copy stream waits on the
+            # root's event) and after each peer's point where A is final (the
+            # peers' interprocess events); after wait() the peers overwrite A
+            # at once, which must queue behind the root's pulls on the device.
             delay = torch.rand(1536, 1536, device="cuda", dtype=torch.float64)
-            for _ in range(4):
+            for _ in range(8 if me == root else 4):
                 delay = delay @ delay * 1e-3
             A.copy_(final)
+            if me == root:
+                G.zero_()
             h = igg.gather_async_(A, G, root=root)
             busy = torch.rand(256, 256, device="cuda") @ torch.rand(256, 256, device="cuda")  # overlapped work
             h.wait()
-            A.fill_(-1)  # allowed after wait()
+            A.fill_(-1)  # allowed after wait(): device-ordered behind the root's pulls
             torch.cuda.synchronize()
             del busy, delay
             if me == root:
@@ -465,8 +470,15 @@ def scenario_collectives(dev):
         t = torch.arange(7, dtype=torch.float64, device=device) * (me + 1)
         comm.bcast_(t, root=root)
         assert torch.equal(t.cpu(), torch.arange(7, dtype=torch.float64) * (root + 1)), (root, t)
+    if dev != "cpu":  # complex tensors reduce as real pairs
+        t = torch.full((3,), complex(me + 1, -(me + 1)), dtype=torch.complex64, device=device)
+        comm.allreduce_(t, "sum")
+        assert (t.cpu() == complex(n * (n + 1) // 2, -(n * (n + 1) // 2))).all(), t
     r = comm.allreduce(float(me), "max")
     assert r == float(n - 1), r
+    # one RCCL communicator per rank: GPU collectives ride the grid's native
+    # communicator, no torch nccl process group is created next to it
+    assert comm.torch_nccl is None
     try:
         comm.allreduce_(torch.zeros(1), "mean")
         raise AssertionError("expected IGGError for an unknown op")

@@ -18,6 +18,40 @@ def _env(**kw):
     return env
 
 
+def _run(args, timeout=150, **env):
+    r = subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout,
+                       env=_env(**env), cwd=ROOT)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_metric_label_says_what_value_is(n):
+    """The metric label states the value's semantics (whole-job aggregate), and
+    the value is n_gpus x the per-GPU T_eff (also at N=1)."""
+    r, rec = _run(["--gpus", str(n), "--device", "cpu", "--n", "20", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert rec["metric"].startswith("effective GB/s per GPU + weak-scaling parallel efficiency")  # BASELINE.json
+    assert "whole-job aggregate" in rec["metric"] and "sum of the per-GPU T_eff" in rec["metric"]
+    assert "aggregate" in rec["unit"]
+    assert abs(rec["value"] - n * rec["config"]["t_eff_per_gpu_GBs"]) <= 1e-3 * rec["value"] + 0.01
+    if n > 1:  # the post-timing validation ran on every multi-rank run
+        assert rec["config"]["post_validation"]["result"] == "ok", rec["config"]["post_validation"]
+    else:
+        assert rec["config"]["post_validation"] is None
+
+
+def test_post_validation_fails_closed():
+    """A mismatch in the post-timing validation (injected on rank 0) leaves no
+    schedule to fall back to in the CPU plumbing mode: the bench fails and
+    prints no number."""
+    r, rec = _run(["--gpus", "2", "--device", "cpu", "--n", "20", "--steps", "3", "--warmup", "1"],
+                  IGG_BENCH_INJECT="post_validation")
+    assert r.returncode != 0
+    assert rec is None
+    assert "post-timing validation failed" in r.stderr
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_self_launch_reports_n_gpus(n):
     r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--device", "cpu", "--n", "24", "--steps", "4",

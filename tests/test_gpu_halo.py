@@ -448,4 +448,5 @@ def test_gpu_tensor_collectives_single_rank(gpu):
     assert torch.equal(comm.allreduce_(t, "sum").cpu(), torch.arange(4, dtype=torch.float64))
     assert torch.equal(comm.bcast_(t, 0).cpu(), torch.arange(4, dtype=torch.float64))
     assert comm.allreduce(3.5, "max") == 3.5
+    assert comm.torch_nccl is None  # no second (torch) RCCL communicator
     igg.finalize_global_grid(finalize_MPI=False)
