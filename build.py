@@ -8,7 +8,12 @@ snapshot to the GPU box. Incremental: objects are rebuilt only when a source or
 any header is newer. No torch headers are used (the runtime takes raw
 pointers), so a full build takes seconds.
 
-Usage: ``python build.py [--clean] [-j N] [--debug] [--asan]``
+Usage: ``python build.py [--clean] [-j N] [--debug] [--asan] [--probes]``
+
+``--probes`` also compiles the measurement-only kernel forms of rounds 1-2
+(stencil tilings and fused variants that lost their A/B, timing probes whose
+results are wrong on purpose); the default build holds only what the autotune
+shortlist, the fused A/B and their fallbacks use.
 """
 from __future__ import annotations
 
@@ -64,14 +69,17 @@ def _compile(src: Path, obj: Path, flags: list[str]) -> tuple[Path, str]:
     return obj, r.stderr
 
 
-def build(jobs: int | None = None, debug: bool = False, asan: bool = False, verbose: bool = False) -> Path:
+def build(jobs: int | None = None, debug: bool = False, asan: bool = False, verbose: bool = False,
+          probes: bool = False) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
     flags = ["-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-result"]
     flags += ["-O0", "-g"] if debug else ["-O3"]
     if asan:
         # Host-code sanitizer only (GPU ASan is not available on the pool).
         flags += ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
-    tag = ("dbg" if debug else "opt") + ("-asan" if asan else "")
+    if probes:
+        flags += ["-DIGG_PROBES"]
+    tag = ("dbg" if debug else "opt") + ("-asan" if asan else "") + ("-probes" if probes else "")
     hdr_t = _headers_mtime()
     todo = []
     objs = []
@@ -88,7 +96,9 @@ def build(jobs: int | None = None, debug: bool = False, asan: bool = False, verb
                     print(err, file=sys.stderr)
     out = ext_path()
     newest = max(o.stat().st_mtime for o in objs)
-    if not out.exists() or out.stat().st_mtime < newest or todo:
+    stamp = BUILD / "last_link_tag"
+    same_tag = stamp.exists() and stamp.read_text() == tag
+    if not out.exists() or out.stat().st_mtime < newest or todo or not same_tag:
         link = [
             str(ROCM / "bin" / "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}",
             *map(str, objs), "-o", str(out) + ".tmp",
@@ -100,6 +110,7 @@ def build(jobs: int | None = None, debug: bool = False, asan: bool = False, verb
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{' '.join(link)}\n{r.stdout}\n{r.stderr}")
         os.replace(str(out) + ".tmp", out)
+        stamp.write_text(tag)
     return out
 
 
@@ -109,12 +120,13 @@ def main() -> None:
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan", action="store_true")
+    ap.add_argument("--probes", action="store_true", help="also compile the measurement-only kernel forms")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     if a.clean:
         shutil.rmtree(BUILD, ignore_errors=True)
         ext_path().unlink(missing_ok=True)
-    out = build(a.j, a.debug, a.asan, a.verbose)
+    out = build(a.j, a.debug, a.asan, a.verbose, a.probes)
     print(f"built {out.relative_to(ROOT)}")
 
 

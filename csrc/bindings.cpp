@@ -566,8 +566,8 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
         py::arg("stream") = 0, py::arg("rounds") = 0);
   // Inner-box sweep through one restrict-form tiling id (fused_kernels.hip
-  // dispatch_plain), incl. the timing-probe tilings 130-132 whose results
-  // are wrong on purpose (benchmarks/refetch_probe.py).
+  // dispatch_plain); the measurement-only tilings (incl. the timing probes
+  // 130-132 of benchmarks/refetch_probe.py) exist only in a --probes build.
   m.def("diffusion3d_hx_tiling",
         [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
            double dtlam, int elem_bytes, int tiling, uintptr_t stream, int rounds) {
@@ -577,6 +577,15 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
         py::arg("elem_bytes"), py::arg("tiling"), py::arg("stream") = 0, py::arg("rounds") = 0);
   m.def("diffusion3d_fused_variant_ok", &diffusion3d_fused_variant_ok);
+  m.def("diffusion3d_variant_compiled", &stencil_variant_compiled,
+        "Whether stencil variant v is compiled in this build (measurement-only ones: build.py --probes).");
+  m.def("probes_build", []() {
+#ifdef IGG_PROBES
+    return true;
+#else
+    return false;
+#endif
+  });
   m.def("fused_debug", [](uintptr_t stamps, int force_sel) {
     fused_debug(reinterpret_cast<int64_t*>(stamps), force_sel);
   }, py::arg("stamps"), py::arg("force_sel") = -1);

@@ -136,6 +136,11 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
          int64_t clip_hi = INT64_MAX) {
   using V = typename Vec<T, VZ>::type;
   constexpr int W = 64 * VZ * BZ;
+  // FEAT 16384 / 32768 / 65536 / 131072 are measurement-only forms (rounds
+  // 1-2, not adopted): compiled only with build.py --probes (IGG_PROBES).
+#ifndef IGG_PROBES
+  static_assert((FEAT & (16384 | 32768 | 65536 | 131072)) == 0, "measurement-only FEAT bits need IGG_PROBES");
+#endif
   // FEAT 65536 (RV, plain sweeps only): reversed march - chunks from the top x
   // down and each chunk's planes from high x to low - for every other step of
   // the ping-pong loop, so a step starts on the planes the previous (forward)
@@ -291,8 +296,6 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   }
   const T two = T(2);
   T evn = T(0);
-  // FEAT 16384 / 32768: timing probes only (results WRONG): skip the z-segment
-  // edge loads / the y-halo row loads, to price the tile-edge re-fetch.
   if constexpr ((FEAT & 512) != 0 && (FEAT & 16384) == 0) evn = t[xf * s0 + rowe];
   int64_t x = xf;
   for (int64_t i = 0; i < len; ++i, x += DX) {
@@ -302,9 +305,12 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
       evc = evn;
       if constexpr ((FEAT & 16384) == 0) {
         if (i + 1 < len) evn = t[off + DX * s0 + rowe];
-      } else {
-        evn = evn * T(0.5);
       }
+#ifdef IGG_PROBES
+      // FEAT 16384 / 32768: timing probes (results WRONG): skip the z-segment
+      // edge loads / the y-halo row loads, to price the tile-edge re-fetch.
+      if constexpr ((FEAT & 16384) != 0) evn = evn * T(0.5);
+#endif
     }
     // z halo of plane x (fetched one step ahead), prefetch plane x+1's. (The
     // alternative of substituting it at its use measured slower for every
@@ -357,10 +363,13 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     if constexpr ((FEAT & 32768) == 0) {
       ym = vld<T, VZ>(ymb + x * yms + zl);
       yp = vld<T, VZ>(ypb + x * yps + zl);
-    } else {
+    }
+#ifdef IGG_PROBES
+    if constexpr ((FEAT & 32768) != 0) {  // timing probe (results WRONG)
       ym = tc[0];
       yp = tc[RY - 1];
     }
+#endif
     T em[RY], ep[RY];
     if constexpr ((FEAT & 512) == 0) {
 #pragma unroll
@@ -417,10 +426,13 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
       if (r < nv) {
         T* dst = t2 + off + rowb[r] + zl;
         if (lane_full) {
+#ifdef IGG_PROBES
           // FEAT 131072: plain (temporal) stores, to measure what the
           // non-temporal hint costs or saves in the Infinity Cache
           if constexpr ((FEAT & 131072) != 0) *reinterpret_cast<V*>(dst) = out;
-          else __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
+          else
+#endif
+          __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
         } else {
 #pragma unroll
           for (int e = 0; e < VZ; ++e)

@@ -36,6 +36,8 @@ struct DiffusionArgs {
 
 // Number of tuned kernel variants (see stencil_kernels.hip); variant 0 = default.
 int diffusion3d_num_variants();
+// Whether variant v is compiled in this build (measurement-only forms need build.py --probes).
+bool stencil_variant_compiled(int v);
 const char* diffusion3d_variant_name(int v);
 // Width (points along dim 2) of one workgroup tile of variant v.
 int diffusion3d_variant_tile(int v);

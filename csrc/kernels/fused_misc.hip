@@ -8,7 +8,9 @@ namespace {
 template <typename T>
 bool dispatch_misc(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s) {
   switch (v) {
+#ifdef IGG_PROBES  // measured, not adopted
     case 2: launch_mode<T, 4, 4, 2, true, 1>(d, io, mode, s); break;
+#endif
     case 9: launch_mode<T, 4, 8, 4, false, 1>(d, io, mode, s); break;
     case 14: launch_mode<T, 2, 8, 4, false, 2>(d, io, mode, s); break;
     // + edge-lane z exchange (FEAT 8192: no per-row v_readlane, which the

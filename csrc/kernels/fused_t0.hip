@@ -10,7 +10,9 @@ bool dispatch_t0(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, 
   switch (v) {
     case 0: launch_mode<T, 4, 4, 4, false, 1>(d, io, mode, s); break;
     case 50: launch_mode<T, 4, 4, 4, false, 1, 1024>(d, io, mode, s); break;  // tiling 0, one WG per CU
+#ifdef IGG_PROBES  // measured, not adopted
     case 45: launch_mode<T, 4, 4, 4, false, 1, 8192>(d, io, mode, s); break;  // tiling 0 + edge-lane z
+#endif
     default: return false;
   }
   return true;

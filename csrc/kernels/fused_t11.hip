@@ -8,9 +8,13 @@ namespace {
 template <typename T>
 bool dispatch_t11(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s) {
   switch (v) {
+#ifdef IGG_PROBES  // measured, not adopted
     case 11: launch_mode<T, 4, 8, 2, false, 1>(d, io, mode, s); break;
+#endif
     case 40: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024>(d, io, mode, s); break;
+#ifdef IGG_PROBES  // measured, not adopted
     case 41: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024 | 4096>(d, io, mode, s); break;
+#endif
     case 42: launch_mode<T, 4, 8, 2, false, 1, 512 | 1024 | 8192>(d, io, mode, s); break;  // 40 + edge-lane z
     default: return false;
   }

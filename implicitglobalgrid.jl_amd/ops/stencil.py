@@ -22,7 +22,22 @@ _autotune_cache: dict = {}
 
 
 def variants() -> list[str]:
+    """Names of every variant index (measurement-only ones included)."""
     return list(native.diffusion3d_variants())
+
+
+def compiled_variants() -> list[int]:
+    """Variant indices compiled in this build (``build.py --probes`` adds the
+    measurement-only tilings of rounds 1-2)."""
+    return [v for v in range(len(variants())) if native.diffusion3d_variant_compiled(v)]
+
+
+FUSED_VARIANTS = (0, 2, 9, 11, 14, 40, 41, 42, 44, 45, 50)
+
+
+def compiled_fused_variants() -> list[int]:
+    """Fused-exchange variants compiled in this build."""
+    return [v for v in FUSED_VARIANTS if native.diffusion3d_fused_variant_ok(v)]
 
 
 def _check(T2, T, Cp):
@@ -73,7 +88,7 @@ def time_variants(T2, T, Cp, rd2, dtlam, boxes, candidates=None, reps: int = 5, 
     a variant index or a (variant, grid_rounds) pair (grid residency rounds of
     the launch, see diffusion3d_)."""
     n = list(T.shape)
-    cands = list(range(len(variants()))) if candidates is None else list(candidates)
+    cands = compiled_variants() if candidates is None else list(candidates)
     s = torch.cuda.current_stream()
     times = {c: [] for c in cands}
 

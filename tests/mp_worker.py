@@ -491,6 +491,57 @@ def scenario_collectives(dev):
 
 
 
+def scenario_suite(*items):
+    """Several scenarios in ONE launch of the ranks (the multigpu tier's time
+    budget: one process start, one torch import and one rendezvous per suite
+    instead of per check). ``items``: "name:arg:arg|VAR=val;VAR=val" - the
+    scenario's env vars are set for it only. The grid is re-initialised per
+    item on the same process group (init_MPI / finalize_MPI false in between).
+    Progress lines name every item, so a hang or failure is attributable."""
+    import time
+
+    import torch.distributed as dist
+
+    orig_init, orig_fin = igg.init_global_grid, igg.finalize_global_grid
+
+    def init(*a, **k):
+        k.setdefault("init_MPI", not dist.is_initialized())
+        return orig_init(*a, **k)
+
+    def fin(*a, **k):
+        k.setdefault("finalize_MPI", False)
+        return orig_fin(*a, **k)
+
+    igg.init_global_grid, igg.finalize_global_grid = init, fin
+    me = int(os.environ.get("RANK", "0"))
+    t_all = time.time()
+    for item in items:
+        spec, _, envs = item.partition("|")
+        name, *args = spec.split(":")
+        saved = {}
+        for kv in filter(None, envs.split(";")):
+            k, v = kv.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        t0 = time.time()
+        try:
+            globals()[f"scenario_{name}"](*args)
+        except BaseException as e:
+            print(f"rank {me} suite item {item!r} FAILED: {type(e).__name__}: {e}", flush=True)
+            raise
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        print(f"rank {me} suite item {item!r} OK in {time.time() - t0:.1f} s", flush=True)
+    igg.init_global_grid, igg.finalize_global_grid = orig_init, orig_fin
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    print(f"rank {me} suite OK ({len(items)} items, {time.time() - t_all:.1f} s)", flush=True)
+
+
 if __name__ == "__main__":
     name, *args = sys.argv[1:]
     globals()[f"scenario_{name}"](*args)

@@ -115,3 +115,26 @@ def test_driver_torchrun_launch_form():
     assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1
     assert rec["config"]["self_launched"] is False
     assert rec["config"]["parallelism"] == "spatial 2x1x1"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inject", ["", "fused_post"])
+def test_share_gpu_post_timing_checks(inject):
+    """Two ranks on one GPU (put transport, fused exchange): the JSON carries
+    the post-timing transport validation and the post-timing fused check; an
+    injected fused mismatch fails closed (fused dropped, region re-timed on the
+    update_halo_ path, the result still validated)."""
+    r, rec = _run(["--gpus", "2", "--share-gpu", "--fused", "on", "--n", "96", "--steps", "20", "--warmup", "2",
+                   "--launch-timeout", "240"], timeout=280, IGG_BENCH_INJECT=inject,
+                  IGG_FUSED_CANDIDATES="0/8/3,42/12/2", IGG_STENCIL_VARIANT="0")
+    assert r.returncode == 0, r.stderr[-3000:]
+    c = rec["config"]
+    assert c["post_validation"]["result"] == "ok", c["post_validation"]
+    assert c["post_validation"]["transport"] == c["transport"]
+    fp = c["fused_post_check"]
+    assert fp is not None and fp["steps"] >= 200
+    if inject:
+        assert fp["result"] == "mismatch" and "fallback" in fp
+        assert c["fused_halo"] is False
+    else:
+        assert fp["result"] == "ok" and c["fused_halo"] is True

@@ -11,6 +11,9 @@ import torch
 
 import igg
 from igg.models.diffusion3d import Diffusion3D
+from igg.ops import stencil as _stencil
+
+FUSED = _stencil.compiled_fused_variants()  # 2, 11, 41, 45 only in a --probes build
 
 
 def test_fused_unavailable_on_cpu():
@@ -50,7 +53,7 @@ def _pair(n, periods, dtype, variant, loopback=False, mode=0):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("variant", [0, 2, 9, 11, 14, 40, 41, 42, 44, 45, 50])
+@pytest.mark.parametrize("variant", FUSED)
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_fused_periodic_matches_update_halo(gpu, variant, dtype, mode):
     a, b = _pair((34, 29, 136), (1, 1, 1), dtype, variant, mode=mode)
@@ -78,7 +81,7 @@ def test_fused_partial_periodic(gpu, periods):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [2, 3])
-@pytest.mark.parametrize("variant", [0, 2, 9, 11, 14, 40, 41, 42, 44, 45, 50])
+@pytest.mark.parametrize("variant", FUSED)
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("periods", [(1, 1, 0), (1, 1, 1)])
 def test_fused_no_z_exchange_matches_update_halo(gpu, variant, dtype, mode, periods):
@@ -97,7 +100,7 @@ def test_fused_no_z_exchange_matches_update_halo(gpu, variant, dtype, mode, peri
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [4, 5])
-@pytest.mark.parametrize("variant", [0, 2, 9, 11, 14, 40, 41, 42, 44, 45, 50])
+@pytest.mark.parametrize("variant", FUSED)
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("periods", [(1, 1, 1), (0, 0, 1), (1, 0, 1)])
 def test_fused_direct_z_matches_update_halo(gpu, variant, dtype, mode, periods):

@@ -2,10 +2,28 @@
 
 Only these tests exercise what single-GPU runs cannot: RCCL point-to-point
 between devices over xGMI, IPC mappings of another device's memory (put
-transport, fused exchange, async gather pulls) and cross-device memory
-ordering. Every test is skipped when fewer GPUs than ranks are visible, so the
-tier collects and skips cleanly on a 1-GPU box; run it on a node with
-``python -m pytest tests -m multigpu``.
+transport, fused exchange, gather pulls) and cross-device memory ordering
+(docs/COHERENCE.md). Every test is skipped when fewer GPUs than ranks are
+visible, so the tier collects and skips cleanly on a 1-GPU box; run it on a
+node with ``python -m pytest tests -m multigpu``.
+
+First-run-proof budget: the checks are chained into suites, one launch of the
+ranks per suite (tests/mp_worker.py scenario_suite: one torch import and one
+rendezvous per launch, the grid re-initialised per item), and every launch is
+bounded by tests/_mp.py MAX_TIMEOUT = 170 s (fail-fast: the first failing rank
+stops the others and names the item). The tier is 10 launches:
+
+    1  8-rank direct-z fused soak (first: the least proven path the bench may pick)
+    2  8-rank fused exchange forms + diffusion vs the global-grid run
+    3  8-rank halo oracle (RCCL sequential / one-phase / auto, put) + ring
+    4  8-rank gather (pull and RCCL paths, roots 0 and 7) + gather_async + collectives
+    5  2-rank suite (left == right periodic neighbour: same-peer ordering; fused)
+    6  4-rank suite (2x2x1)
+    7, 8  bench.py --gpus 2 / --gpus 8 self-launch (validation + post-timing checks)
+    9, 10 2- and 4-rank direct-z fused soak
+
+Worst case (every launch hitting its bound): 10 x 170 s = 28.3 min; expected
+on a healthy node: about 3-4 min (each suite item takes seconds).
 
 Reference counterparts: test/test_update_halo.jl (halo oracle incl. dims=2
 periodic, where left == right neighbour), :697-743 (ring), test/test_gather.jl
@@ -18,7 +36,7 @@ import sys
 
 import pytest
 
-from tests._mp import ROOT, run_ranks
+from tests._mp import MAX_TIMEOUT, ROOT, run_ranks
 
 pytestmark = [pytest.mark.gpu, pytest.mark.multigpu]
 
@@ -37,100 +55,123 @@ def need(n: int):
         pytest.skip(f"needs {n} GPUs (one rank per device), {_ngpus()} visible")
 
 
-MGPU = {"IGG_TEST_DEV": "mgpu"}
-RCCL = {**MGPU, "IGG_TRANSPORT": "rccl"}
-PUT = {**MGPU, "IGG_TRANSPORT": "put", "IGG_PUT_TIMEOUT": "20"}
+MGPU = "IGG_TEST_DEV=mgpu"
+RCCL = f"{MGPU};IGG_TRANSPORT=rccl"
+PUT = f"{MGPU};IGG_TRANSPORT=put;IGG_PUT_TIMEOUT=20"
 
 
-@pytest.mark.parametrize("mode", ["sequential", "onephase", "auto"])
-@pytest.mark.parametrize("nprocs,cfg", [
-    (2, (7, 5, 6, 1, 1, 1)),   # 2x1x1 periodic: left == right neighbour (same-peer ordering)
-    (2, (7, 5, 6, 0, 0, 0)),
-    (4, (9, 6, 5, 1, 0, 1)),   # 2x2x1
-    (8, (7, 5, 6, 0, 0, 0)),   # 2x2x2
-    (8, (7, 5, 6, 1, 1, 1)),   # 2x2x2 periodic: every direction is a neighbour (edges, corners)
-])
-def test_halo_rccl_across_devices(nprocs, cfg, mode):
+def fused(v, mode, *cfg):
+    """Fused exchange (stencil stores its send planes over xGMI) vs stencil +
+    update_halo_ (RCCL), bitwise on every rank."""
+    return f"diffusion_fused:{':'.join(map(str, cfg))}|{RCCL};IGG_PUT_TIMEOUT=20;IGG_TEST_VARIANT={v};" \
+           f"IGG_TEST_FUSED_MODE={mode}"
+
+
+def soak(v, mode, rounds=40, per=40):
+    return f"fused_soak:20:18:32:{rounds}:{per}|{PUT};IGG_PUT_TIMEOUT=30;IGG_TEST_VARIANT={v};" \
+           f"IGG_TEST_FUSED_MODE={mode}"
+
+
+def halo(cfg, env):
+    return f"halo:mgpu:{':'.join(map(str, cfg))}:f64|{env}"
+
+
+def suite(nprocs, *items):
     need(nprocs)
-    run_ranks(nprocs, "halo", "mgpu", *cfg, "f64", env_extra={**RCCL, "IGG_HALO_MODE": mode})
+    outs = run_ranks(nprocs, "suite", *items, timeout=MAX_TIMEOUT)
+    for o in outs:
+        assert f"suite OK ({len(items)} items" in o, o[-3000:]
 
 
-@pytest.mark.parametrize("nprocs,cfg", [(2, (7, 5, 6, 1, 1, 1)), (4, (9, 6, 5, 1, 0, 1)), (8, (7, 5, 6, 1, 1, 1))])
-def test_halo_put_across_devices(nprocs, cfg):
-    need(nprocs)
-    run_ranks(nprocs, "halo", "mgpu", *cfg, "f64", env_extra=PUT)
+# 1. the direct-z fused soak first (direct z: the z faces land in the halo
+#    column of the neighbour's next field; random host skew between rounds)
+def test_direct_z_fused_soak_8_ranks():
+    suite(8, soak(40, 4), soak(42, 12), soak(0, 1))
 
 
-@pytest.mark.parametrize("nprocs", [2, 4, 8])
-def test_ring_rccl(nprocs):
-    need(nprocs)
-    run_ranks(nprocs, "ring", "mgpu", env_extra=RCCL)
+# 2. fused exchange forms and the 8-rank diffusion vs one global array
+def test_fused_forms_and_diffusion_8_ranks():
+    suite(8,
+          fused(0, 1, 18, 20, 40, 7, 0, 0),
+          fused(0, 0, 16, 18, 24, 6, 1, 1),
+          fused(42, 4, 18, 20, 136, 5, 0, 1),
+          fused(0, 5, 16, 18, 24, 6, 1, 1),
+          fused(40, 8, 34, 66, 136, 5, 1, 1),
+          fused(44, 4, 18, 20, 136, 4, 1, 0),
+          f"diffusion:mgpu:24:20:18:7:0|{RCCL}",
+          f"diffusion:mgpu:24:20:18:7:0|{PUT}")
 
 
-@pytest.mark.parametrize("nprocs", [2, 4, 8])
-def test_gather_rccl_root_first_and_last(nprocs):
-    need(nprocs)
-    run_ranks(nprocs, "gather", "mgpu", "f64", env_extra=RCCL)
+# 3. halo oracle (every boundary plane, edges and corners, bitwise)
+def test_halo_and_ring_8_ranks():
+    items = []
+    for cfg in ((7, 5, 6, 0, 0, 0), (7, 5, 6, 1, 1, 1)):
+        for mode in ("sequential", "onephase", "auto"):
+            items.append(halo(cfg, f"{RCCL};IGG_HALO_MODE={mode}"))
+    items.append(halo((7, 5, 6, 1, 1, 1), PUT))
+    items.append(f"ring:mgpu|{RCCL}")
+    suite(8, *items)
 
 
-@pytest.mark.parametrize("nprocs", [2, 8])
-def test_gather_async_across_devices(nprocs):
-    need(nprocs)
-    run_ranks(nprocs, "gather_async", env_extra=PUT)
+# 4. gather (pull path and RCCL path, roots 0 and N-1), gather_async, collectives
+def test_gather_and_collectives_8_ranks():
+    suite(8,
+          f"gather:mgpu:f64|{RCCL}",
+          f"gather:mgpu:f64|{RCCL};IGG_GATHER_PULL=0",
+          f"gather_async|{PUT}",
+          f"collectives:mgpu|{RCCL}")
 
 
-@pytest.mark.parametrize("transport", ["rccl", "put"])
-def test_diffusion_8_ranks_matches_global(transport):
-    """The 8-rank run (2x2x2) equals the same physics on one global array."""
-    need(8)
-    run_ranks(8, "diffusion", "mgpu", 24, 20, 18, 7, 0, env_extra=RCCL if transport == "rccl" else PUT)
+# 5. two ranks: periodic dims=2 makes left == right (same-peer ordering)
+def test_suite_2_ranks():
+    suite(2,
+          *[halo((7, 5, 6, 1, 1, 1), f"{RCCL};IGG_HALO_MODE={m}") for m in ("sequential", "onephase", "auto")],
+          halo((7, 5, 6, 0, 0, 0), RCCL),
+          halo((7, 5, 6, 1, 1, 1), PUT),
+          f"ring:mgpu|{RCCL}",
+          f"gather:mgpu:f64|{RCCL}",
+          f"gather_async|{PUT}",
+          f"collectives:mgpu|{RCCL}",
+          fused(0, 0, 24, 20, 64, 6, 0, 0),
+          fused(40, 4, 24, 20, 64, 6, 1, 0),
+          fused(42, 12, 40, 66, 136, 6, 1, 0))
 
 
-@pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 0, 0), ("0", "0")),
-                                               (4, (20, 22, 32, 5, 1, 1), ("9", "1")),
-                                               (8, (18, 20, 40, 7, 0, 0), ("0", "1")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("11", "0")),
-                                               # direct z (mode bit 4): z faces stored over xGMI into
-                                               # the halo column of the neighbour's next field
-                                               (2, (24, 20, 64, 6, 1, 0), ("40", "4")),
-                                               (8, (18, 20, 136, 5, 0, 1), ("42", "4")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("0", "5")),
-                                               # peeled x planes (mode bit 8)
-                                               (2, (40, 66, 136, 6, 1, 0), ("42", "12")),
-                                               (8, (34, 66, 136, 5, 1, 1), ("40", "8"))])
-def test_fused_exchange_across_devices(nprocs, cfg, kernel):
-    """Stencil kernel stores its send planes into the neighbours' arenas over
-    xGMI: bitwise equal to stencil + update_halo_ (RCCL) on every rank."""
-    need(nprocs)
-    env = {**RCCL, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
-    run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=170)
+# 6. four ranks (2x2x1)
+def test_suite_4_ranks():
+    suite(4,
+          *[halo((9, 6, 5, 1, 0, 1), f"{RCCL};IGG_HALO_MODE={m}") for m in ("sequential", "onephase", "auto")],
+          halo((9, 6, 5, 1, 0, 1), PUT),
+          f"ring:mgpu|{RCCL}",
+          f"gather:mgpu:f64|{RCCL}",
+          fused(9, 1, 20, 22, 32, 5, 1, 1),
+          f"diffusion:mgpu:24:20:18:5:0|{RCCL}")
 
 
-@pytest.mark.parametrize("nprocs,kernel", [(4, ("0", "1")), (8, ("0", "1")), (8, ("40", "4"))])
-def test_fused_soak_across_devices(nprocs, kernel):
-    need(nprocs)
-    env = {**PUT, "IGG_PUT_TIMEOUT": "30", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
-    run_ranks(nprocs, "fused_soak", 20, 18, 32, 40, 40, env_extra=env, timeout=170)
-
-
-@pytest.mark.parametrize("nprocs", [2, 8])
-def test_tensor_collectives_gpu(nprocs):
-    need(nprocs)
-    run_ranks(nprocs, "collectives", "mgpu", env_extra=RCCL)
-
-
+# 7, 8. the bench on N distinct GPUs
 @pytest.mark.parametrize("nprocs", [2, 8])
 def test_bench_self_launch_validates_every_transport(nprocs):
     """bench.py --gpus N (self-launched, one rank per GPU) validates RCCL
-    sequential / one-phase and put bitwise against the host-staged path and
-    reports n_gpus == N."""
+    sequential / one-phase and put bitwise against the host-staged path before
+    timing, checks the timed schedule (and the fused exchange, if kept) after
+    timing, and reports n_gpus == N."""
     need(nprocs)
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nprocs), "--n", "128",
                         "--steps", "20", "--warmup", "2", "--launch-timeout", "150"],
-                       capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
+                       capture_output=True, text=True, timeout=MAX_TIMEOUT, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    c = rec["config"]
     assert rec["n_gpus"] == nprocs
-    assert rec["config"]["validation"] == {"rccl-sequential": "ok", "rccl-onephase": "ok", "put": "ok"}, rec
-    assert rec["config"]["finite"]
+    assert c["validation"] == {"rccl-sequential": "ok", "rccl-onephase": "ok", "put": "ok"}, rec
+    assert c["post_validation"]["result"] == "ok", c["post_validation"]
+    if c["fused_halo"]:
+        assert c["fused_post_check"]["result"] == "ok", c["fused_post_check"]
+    assert c["finite"]
+
+
+# 9, 10. direct-z soak at 2 and 4 ranks
+@pytest.mark.parametrize("nprocs", [2, 4])
+def test_direct_z_fused_soak_small(nprocs):
+    suite(nprocs, soak(40, 4, rounds=30), soak(0, 5, rounds=30))

@@ -149,3 +149,28 @@ def test_barrier_timeout_raises_instead_of_hanging():
 @pytest.mark.parametrize("nprocs", [2, 4])
 def test_tensor_collectives_cpu(nprocs):
     run_ranks(nprocs, "collectives", "cpu")
+
+
+def test_suite_chains_scenarios_cpu():
+    """The multigpu tier's chained suite (several scenarios per launch, the
+    grid re-initialised on one process group) works; CPU/gloo ranks here."""
+    outs = run_ranks(2, "suite", "halo:cpu:7:5:6:1:1:1:f64", "gather:cpu:f64", "ring:cpu",
+                     "collectives:cpu", "diffusion:cpu:24:20:18:3:0|IGG_HALO_MODE=sequential", timeout=120)
+    for o in outs:
+        assert "suite OK (5 items" in o, o[-2000:]
+
+
+@pytest.mark.gpu
+def test_suite_chains_scenarios_shared_gpu():
+    """The multigpu tier's suite mechanism on GPU ranks sharing device 0 (put
+    transport; RCCL refuses ranks on one device): direct-z soak, fused forms,
+    halo oracle, pull gather, gather_async in one launch."""
+    dev = "IGG_TEST_DEV=gpu;IGG_TRANSPORT=put;IGG_PUT_TIMEOUT=20"
+    outs = run_ranks(2, "suite",
+                     f"fused_soak:20:18:32:10:20|{dev};IGG_TEST_VARIANT=40;IGG_TEST_FUSED_MODE=4",
+                     f"diffusion_fused:24:20:64:6:1:0|{dev};IGG_TEST_VARIANT=42;IGG_TEST_FUSED_MODE=12",
+                     f"halo:gpu:7:5:6:1:1:1:f64|{dev}",
+                     f"gather:gpu:f64|{dev}",
+                     f"gather_async|{dev}", timeout=160, env_extra={"GPU_MAX_HW_QUEUES": "1"})
+    for o in outs:
+        assert "suite OK (5 items" in o, o[-2000:]
