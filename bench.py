@@ -461,6 +461,12 @@ def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = 
     import torch
 
     model.set_fused(False)
+    # The reference is the serial update_halo_ step: an overlapped schedule
+    # (boundary slabs by another kernel variant) is not bitwise comparable
+    # with the fused kernel in every dtype (f32 contraction differs).
+    ov = bool(getattr(model, "overlap", False))
+    if ov:
+        model.set_overlap(False)
     T0, T20 = model.T.clone(), model.T2.clone()
     model.run(nchk)
     ref = model.T.clone()
@@ -488,6 +494,8 @@ def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = 
     model.T.copy_(T0)
     model.T2.copy_(T20)
     model.fused, model._fprimed, model.graph = False, False, None  # T was restored: halos valid
+    if ov:
+        model.set_overlap(True)
     del ref, T0, T20
     return bad == 0.0
 

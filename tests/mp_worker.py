@@ -25,6 +25,12 @@ def _device(kind):
     return torch.device("cpu")
 
 
+def _plain(v: int) -> int:
+    """Plain stencil variant for a fused-variant id (the fused ids reuse the
+    plain index space; a fused-only or measurement-only id maps to 0)."""
+    return v if igg.native.diffusion3d_variant_compiled(v) else 0
+
+
 def scenario_halo(dev, nx, ny, nz, px, py, pz, dt, dimx=0, dimy=0, dimz=0):
     device = _device(dev)
     nx, ny, nz, px, py, pz = map(int, (nx, ny, nz, px, py, pz))
@@ -144,11 +150,12 @@ def scenario_diffusion_fused(nx, ny, nz, steps, periodic, graph):
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, periodx=per, periody=per, periodz=per,
                                                           quiet=True, select_device=False)
     v = int(os.environ.get("IGG_TEST_VARIANT", "0"))
-    a = Diffusion3D(dtype=torch.float64, device=device, variant=v)
-    b = Diffusion3D(dtype=torch.float64, device=device, variant=v)
+    a = Diffusion3D(dtype=torch.float64, device=device, variant=_plain(v))
+    b = Diffusion3D(dtype=torch.float64, device=device, variant=_plain(v))
     b.fused_variant, b.fused_mode = v, int(os.environ.get("IGG_TEST_FUSED_MODE", "0"))
     want = b.fused_mode
     assert b.set_fused(True), "fused mode unavailable"
+    assert b.fused_variant == v, f"fused variant {v} is not compiled in this build"
     assert b.fused_mode == want, f"send mode {want} unavailable (direct z needs the peers' field buffers)"
     a.run(steps)
     if int(graph):
@@ -268,8 +275,8 @@ def scenario_fused_soak(nx, ny, nz, rounds, per_round):
     me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, periodx=1, periody=1, periodz=1,
                                                           quiet=True, select_device=False)
     v = int(os.environ.get("IGG_TEST_VARIANT", "0"))
-    a = Diffusion3D(dtype=torch.float64, device=device, variant=v)
-    b = Diffusion3D(dtype=torch.float64, device=device, variant=v)
+    a = Diffusion3D(dtype=torch.float64, device=device, variant=_plain(v))
+    b = Diffusion3D(dtype=torch.float64, device=device, variant=_plain(v))
     b.fused_variant, b.fused_mode = v, int(os.environ.get("IGG_TEST_FUSED_MODE", "0"))
     assert b.set_fused(True)
     b.step()

@@ -42,12 +42,14 @@ def _pair(n, periods, dtype, variant, loopback=False, mode=0):
         H.enable_loopback()
     from igg.ops import stencil
 
-    # fused-only ids (50-52: tiling 0 forms) have no plain variant
-    plain = variant if variant < len(stencil.variants()) else 0
+    # fused ids reuse the plain index space; fused-only / measurement-only ids
+    # (e.g. 50: a tiling 0 form) run the plain step with variant 0
+    plain = variant if variant in stencil.compiled_variants() else 0
     a = Diffusion3D(dtype=dtype, variant=plain)
     b = Diffusion3D(dtype=dtype, variant=plain)
     b.fused_variant, b.fused_mode = variant, mode
     assert b.set_fused(True)
+    assert b.fused_variant == variant, f"fused variant {variant} is not compiled in this build"
     return a, b
 
 
@@ -70,7 +72,7 @@ def test_fused_periodic_matches_update_halo(gpu, variant, dtype, mode):
 @pytest.mark.parametrize("periods", [(1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 0), (0, 1, 1)])
 def test_fused_partial_periodic(gpu, periods):
     """Only some sides have a neighbour; the others keep their boundary values."""
-    a, b = _pair((21, 19, 64), periods, torch.float64, 11, mode=int(sum(periods) == 1))
+    a, b = _pair((21, 19, 64), periods, torch.float64, 40, mode=int(sum(periods) == 1))
     a.run(6)
     b.run(6)
     b.sync_halo()
@@ -159,7 +161,7 @@ def test_fused_direct_z_graph(gpu):
 def test_fused_loopback_graph_and_mode_switches(gpu):
     """Loopback grid, hipGraph replays with odd/even step counts, sync_halo in
     between (re-primes from the field) and switching back to update_halo_."""
-    a, b = _pair((40, 36, 72), (1, 1, 1), torch.float64, 2, loopback=True, mode=1)
+    a, b = _pair((40, 36, 72), (1, 1, 1), torch.float64, 9, loopback=True, mode=1)
     a.run(3)
     b.run(3)
     b.capture(steps=4)  # counter odd: the graph bakes in that parity

@@ -112,7 +112,7 @@ def test_gather_async_gpu(nprocs):
 @pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 0, 0), ("0", "0")),
                                                (4, (20, 22, 32, 5, 1, 1), ("9", "1")),
                                                (8, (18, 20, 40, 7, 0, 0), ("0", "1")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("11", "0")),
+                                               (8, (16, 18, 24, 6, 1, 1), ("50", "0")),
                                                # per-side wave classes of variant 40 and the edge-lane z
                                                # form of 42 (n2 > 64*VZ+VZ) on one-sided (non-periodic) ranks
                                                (4, (20, 22, 136, 5, 0, 0), ("40", "0")),
