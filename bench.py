@@ -452,14 +452,27 @@ def _inject(what: str) -> bool:
     return what in os.environ.get("IGG_BENCH_INJECT", "").split(",") and int(global_grid().me) == 0
 
 
+def _state(model) -> list[str]:
+    """Names of the model fields a time step evolves (compared bitwise)."""
+    return ["P", "Vx", "Vy", "P2", "Vx2", "Vy2"] if hasattr(model, "Vx") else ["T", "T2"]
+
+
+def _fused_name(model) -> str:
+    if hasattr(model, "fused_variant"):
+        return f"v{model.fused_variant}/m{model.fused_mode}/r{model.fused_rounds}"
+    return "fused"
+
+
 def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = "") -> bool:
-    """Bitwise check of the model's CURRENT fused kernel (variant / send mode /
-    grid rounds) against the update_halo_ path: ``nchk`` steps from the same
-    state on every rank, in the timed run's execution shape (a primed arena,
-    hipGraph replays of captured fused steps plus eager steps for the parity).
-    Collective; every rank agrees. The model's state is restored."""
+    """Bitwise check of the model's CURRENT fused exchange (diffusion: variant /
+    send mode / grid rounds; acoustic: the fused staggered step) against the
+    update_halo_ path: ``nchk`` steps from the same state on every rank, in the
+    timed run's execution shape (hipGraph replays of captured fused steps plus
+    eager steps for the parity). Collective; every rank agrees. The model's
+    state is restored (by content)."""
     import torch
 
+    names = _state(model)
     model.set_fused(False)
     # The reference is the serial update_halo_ step: an overlapped schedule
     # (boundary slabs by another kernel variant) is not bitwise comparable
@@ -467,11 +480,15 @@ def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = 
     ov = bool(getattr(model, "overlap", False))
     if ov:
         model.set_overlap(False)
-    T0, T20 = model.T.clone(), model.T2.clone()
+    saved = {n: getattr(model, n).clone() for n in names}
+
+    def restore():
+        for n in names:
+            getattr(model, n).copy_(saved[n])
+
     model.run(nchk)
-    ref = model.T.clone()
-    model.T.copy_(T0)
-    model.T2.copy_(T20)
+    ref = {n: getattr(model, n).clone() for n in names}
+    restore()
     ok = False
     try:
         model.set_fused(True)
@@ -479,77 +496,89 @@ def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = 
         model.capture(steps=4)
         model.run(nchk - 1)
         model.graph = None
-        model.sync_halo()
+        if hasattr(model, "sync_halo"):
+            model.sync_halo()
         _sync(comm)
         model.check()
         if inject and _inject(inject):
-            model.T.view(-1)[model.T.numel() // 2] += 1
-        ok = bool(torch.equal(ref, model.T))
+            t = getattr(model, names[0])
+            t.view(-1)[t.numel() // 2] += 1
+        ok = all(bool(torch.equal(ref[n], getattr(model, n))) for n in names)
     except Exception as e:  # e.g. a sync kernel timed out: this fused kernel does not work here
-        log(f"fused check v{model.fused_variant}/m{model.fused_mode}/r{model.fused_rounds} failed: "
-            f"{type(e).__name__}: {e}"[:300])
+        log(f"fused check {_fused_name(model)} failed: {type(e).__name__}: {e}"[:300])
         if getattr(comm, "mesh", None) is not None:
             comm.mesh.clear_error()
     bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
-    model.T.copy_(T0)
-    model.T2.copy_(T20)
-    model.fused, model._fprimed, model.graph = False, False, None  # T was restored: halos valid
+    restore()
+    model.fused, model.graph = False, None
+    if hasattr(model, "_fprimed"):
+        model._fprimed = False  # T was restored: halos valid
     if ov:
         model.set_overlap(True)
-    del ref, T0, T20
+    del ref, saved
     return bad == 0.0
 
 
 def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None:
-    """Fused halo exchange (stencil stores the send planes into the neighbours'
-    arenas; igg/fused.hpp) vs the schedule chosen so far: bitwise check of 24
-    steps from the same state on every rank, A/B timing of the candidates (MAX
-    over ranks), then the same bitwise check of the candidate that is kept
-    (falling back to the next fastest that passes).
-    ``mode``: auto (keep the faster), on (force when it checks out), off."""
+    """Fused halo exchange (the kernel stores its send planes / faces into the
+    neighbours' memory; igg/fused.hpp, igg/acoustic.hpp) vs the schedule chosen
+    so far: bitwise check of 24 steps from the same state on every rank, A/B
+    timing of the candidates (MAX over ranks), then a 200-step bitwise check
+    of the candidate that is kept (falling back to the next fastest that
+    passes). ``mode``: auto (keep the faster), on (force when it checks out), off."""
     if mode == "off" or not getattr(model, "can_fuse", False):
         return None
     if not _fused_check(model, comm, log):
         log("fused halo exchange mismatched the update_halo_ path on some rank: excluded")
         return {"fused_ok": False}
-    # Fused kernel candidates: tiling variant x send mode (0 = stores as
-    # computed, 1 = deferred one x step: robust to slow remote acknowledgements).
-    # Two interleaved passes of 20 steps, best of the two per candidate: the
-    # candidates differ by a few us/step, about the size of one pass's noise.
-    cands = list(FUSED_CANDIDATES)
-    if any(model.sides[2]) and model._fh is not None and model._fh.has_fields:
-        cands += FUSED_DIRECT
-        if model.T.dtype.itemsize == 4:
-            cands += FUSED_DIRECT_F32
-    # every form also with its exchanged x planes peeled off the chunk sweep
-    # (send mode bit 8: profiles/r2_peel/, -1.8 % f64 / -2.8 % f32 interior rank)
-    cands += [(v, fm | 8, gr) for v, fm, gr in cands]
-    if os.environ.get("IGG_FUSED_CANDIDATES"):  # "v/mode/rounds,..." (measurements)
-        cands = [tuple(int(x) for x in c.split("/")) for c in os.environ["IGG_FUSED_CANDIDATES"].split(",")]
+    diffusion = hasattr(model, "fused_variant")
+    if diffusion:
+        # Fused kernel candidates: tiling variant x send mode (0 = stores as
+        # computed, 1 = deferred one x step: robust to slow remote
+        # acknowledgements). Two interleaved passes of 20 steps, best of the
+        # two per candidate: the candidates differ by a few us/step, about the
+        # size of one pass's noise.
+        cands = list(FUSED_CANDIDATES)
+        if any(model.sides[2]) and model._fh is not None and model._fh.has_fields:
+            cands += FUSED_DIRECT
+            if model.T.dtype.itemsize == 4:
+                cands += FUSED_DIRECT_F32
+        # every form also with its exchanged x planes peeled off the chunk sweep
+        # (send mode bit 8: profiles/r2_peel/, -1.8 % f64 / -2.8 % f32 interior rank)
+        cands += [(v, fm | 8, gr) for v, fm, gr in cands]
+        if os.environ.get("IGG_FUSED_CANDIDATES"):  # "v/mode/rounds,..." (measurements)
+            cands = [tuple(int(x) for x in c.split("/")) for c in os.environ["IGG_FUSED_CANDIDATES"].split(",")]
+    else:
+        cands = [None]  # the acoustic step has one fused form
+
+    def use(c):
+        if c is not None:
+            model.fused_variant, model.fused_mode, model.fused_rounds = c
+
+    name = (lambda k: f"v{k[0]}/m{k[1]}/r{k[2]}") if diffusion else (lambda k: "fused")  # noqa: E731
     t_unf, times = float("inf"), {}
     for _ in range(2):
         model.set_fused(False)
         t_unf = min(t_unf, _timed_candidate(model, comm, 20, graph))
         model.set_fused(True)
-        for v, fm, gr in cands:
-            model.fused_variant, model.fused_mode, model.fused_rounds = v, fm, gr
+        for c in cands:
+            use(c)
             t = _timed_candidate(model, comm, 20, graph)
-            times[(v, fm, gr)] = min(times.get((v, fm, gr), float("inf")), t)
+            times[c] = min(times.get(c, float("inf")), t)
     model.set_fused(False)
     model.graph = None
-    name = lambda k: f"v{k[0]}/m{k[1]}/r{k[2]}"  # noqa: E731
     keep, best, rejected = False, None, []
     for cand, t_fus in sorted(times.items(), key=lambda kv: kv[1]):
         if not (mode == "on" or t_fus < t_unf):
             break
-        model.fused_variant, model.fused_mode, model.fused_rounds = cand
+        use(cand)
         # the kept candidate: a long check whatever the quick one said
         if _fused_check(model, comm, log, nchk=FUSED_KEEP_CHECK_STEPS):
             keep, best = True, cand
             break
         rejected.append(name(cand))
     if keep:
-        model.fused_variant, model.fused_mode, model.fused_rounds = best
+        use(best)
     model.set_fused(keep)
     model.graph = None
     log(f"fused A/B (ms/step): update_halo={t_unf * 1e3:.4f}, "
@@ -640,7 +669,7 @@ def main():
         else:
             raise RuntimeError("no device transport passed the bitwise validation")
     fused_ab = None
-    if on_gpu and not is2d and not args.overlap and (nprocs > 1 or args.loopback or pdims):
+    if on_gpu and not args.overlap and (nprocs > 1 or args.loopback or pdims):
         fused_ab = select_fused(model, comm, log, args.fused, graph_ok)
     for _ in range(args.warmup):
         model.step()
@@ -822,8 +851,10 @@ def main():
                 "fused_post_check": fused_post,
                 "transport_ab_ms": ab,
                 "fused_halo": bool(getattr(model, "fused", False)),
-                "fused_kernel": ({"variant": model.fused_variant, "mode": model.fused_mode,
-                                  "grid_rounds": model.fused_rounds} if getattr(model, "fused", False) else None),
+                "fused_kernel": (({"variant": model.fused_variant, "mode": model.fused_mode,
+                                   "grid_rounds": model.fused_rounds} if hasattr(model, "fused_variant")
+                                  else {"acoustic": "fused staggered faces"})
+                                 if getattr(model, "fused", False) else None),
                 "stencil_grid_rounds": getattr(model, "rounds", None),
                 "fused_ab_ms": fused_ab,
                 "stencil_variant": getattr(model, "variant", None),

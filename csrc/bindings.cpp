@@ -544,6 +544,27 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("p2"), py::arg("vx2"), py::arg("vy2"), py::arg("p"), py::arg("vx"), py::arg("vy"), py::arg("nx"),
         py::arg("ny"), py::arg("dtk"), py::arg("dt_rho"), py::arg("rdx"), py::arg("rdy"), py::arg("elem_bytes"),
         py::arg("device"), py::arg("stream") = 0);
+  py::class_<FusedAcoustic, std::shared_ptr<FusedAcoustic>>(m, "FusedAcoustic")
+      .def(py::init([](std::shared_ptr<PeerMesh> mesh, int64_t nx, int64_t ny, int elem_bytes,
+                       const std::array<std::array<int, 2>, 2>& nb) {
+             return std::make_shared<FusedAcoustic>(mesh, nx, ny, elem_bytes, nb);
+           }),
+           py::arg("mesh"), py::arg("nx"), py::arg("ny"), py::arg("elem_bytes"), py::arg("neighbors"))
+      .def("set_fields", &FusedAcoustic::set_fields, py::arg("vx_a"), py::arg("vx_b"), py::arg("vy_a"),
+           py::arg("vy_b"))
+      .def("step",
+           [](FusedAcoustic& f, uintptr_t p2, uintptr_t vx2, uintptr_t vy2, uintptr_t p, uintptr_t vx, uintptr_t vy,
+              int64_t nx, int64_t ny, double dtk, double dt_rho, double rdx, double rdy, int elem_bytes,
+              uintptr_t stream) {
+             TraceRange tr("igg.acoustic2d_fused");
+             AcousticArgs a{p2, vx2, vy2, p, vx, vy, nx, ny, dtk, dt_rho, rdx, rdy, elem_bytes};
+             f.step(a, as_stream(stream));
+           },
+           py::arg("p2"), py::arg("vx2"), py::arg("vy2"), py::arg("p"), py::arg("vx"), py::arg("vy"), py::arg("nx"),
+           py::arg("ny"), py::arg("dtk"), py::arg("dt_rho"), py::arg("rdx"), py::arg("rdy"), py::arg("elem_bytes"),
+           py::arg("stream"))
+      .def("check_error", &FusedAcoustic::check_error)
+      .def("close", &FusedAcoustic::close);
   m.def("acoustic2d_set_variant", &acoustic2d_set_variant);
   m.def("acoustic2d_set_chunk", &acoustic2d_set_chunk);
   m.def("diffusion3d_set_rounds", &diffusion3d_set_rounds);

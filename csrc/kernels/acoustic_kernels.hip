@@ -147,8 +147,29 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_march_kernel(AcousticAr
 // global memory accepts dword-aligned dwordx4), and the lane that starts at
 // column ny handles the last Vy face column with a scalar access. Same
 // arithmetic per element as acoustic2d_march_kernel (bitwise equal).
-template <typename T, int VJ>
-__global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticArgs a, int64_t ch) {
+//
+// FUSED (FusedAcoustic, acoustic.hpp): the staggered boundary faces travel to
+// the neighbours inside this sweep. Row i = 2 of Vx2 goes to the x-low
+// neighbour's row nx, row nx-2 to the x-high neighbour's row 0; column 2 of
+// Vy2 to the y-low neighbour's column ny, column ny-2 to the y-high
+// neighbour's column 0 - system-scope stores (st_sys: written through this
+// XCD's L2, acknowledged by the owner's memory before the wave retires); and
+// this rank's own faces on a side with a neighbour are not written here (the
+// neighbour stores them).
+template <typename T>
+__device__ __forceinline__ void st_sys(T* p, const T& v) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16, "st_sys: 4, 8 or 16 B");
+  if constexpr (sizeof(T) == 16)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+  else if constexpr (sizeof(T) == 8)
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+  else
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+}
+
+template <typename T, int VJ, bool FUSED>
+__global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticArgs a, int64_t ch,
+                                                                     AcousticHalo h) {
   typedef T V __attribute__((ext_vector_type(VJ)));
   typedef T VU __attribute__((ext_vector_type(VJ), aligned(sizeof(T))));
   constexpr int64_t OWNV = 62 * VJ;
@@ -229,10 +250,26 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
 #pragma unroll
           for (int e = 0; e < VJ; ++e) vxo[e] = (i >= 1) ? vx_i[e] - dt_rho * (pc[e] - p2_prev[e]) * rdx : vx_i[e];
           __builtin_nontemporal_store(pc, reinterpret_cast<V*>(p2 + i * ny + j0));
-          __builtin_nontemporal_store(vxo, reinterpret_cast<V*>(vx2 + i * ny + j0));
-          *reinterpret_cast<VU*>(vy2 + i * sy + j0) = vyo;
+          if constexpr (FUSED) {
+            // face 0 of a side with a neighbour: the neighbour stores it
+            if (!(i == 0 && h.nb_x[0])) __builtin_nontemporal_store(vxo, reinterpret_cast<V*>(vx2 + i * ny + j0));
+            if (i == 2 && h.send_x[0]) st_sys(reinterpret_cast<V*>(h.send_x[0]) + j0 / VJ, vxo);
+            if (i == nx - 2 && h.send_x[1]) st_sys(reinterpret_cast<V*>(h.send_x[1]) + j0 / VJ, vxo);
+            if (j0 == 0 && h.nb_y[0]) {  // column 0 is the y-low neighbour's to store
+#pragma unroll
+              for (int e = 1; e < VJ; ++e) vy2[i * sy + e] = vyo[e];
+            } else {
+              *reinterpret_cast<VU*>(vy2 + i * sy + j0) = vyo;
+            }
+            const int64_t r2 = 2 - j0, rn = ny - 2 - j0;  // element of column 2 / ny-2 in this lane
+            if (h.send_y[0] && r2 >= 0 && r2 < VJ) st_sys(reinterpret_cast<T*>(h.send_y[0]) + i * sy, vyo[r2]);
+            if (h.send_y[1] && rn >= 0 && rn < VJ) st_sys(reinterpret_cast<T*>(h.send_y[1]) + i * sy, vyo[rn]);
+          } else {
+            __builtin_nontemporal_store(vxo, reinterpret_cast<V*>(vx2 + i * ny + j0));
+            *reinterpret_cast<VU*>(vy2 + i * sy + j0) = vyo;
+          }
         } else if (last) {
-          vy2[i * sy + ny] = vy_h[0];
+          if (!FUSED || !h.nb_y[1]) vy2[i * sy + ny] = vy_h[0];
         }
       }
       vx_i = vx_n;
@@ -241,9 +278,12 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
       vx_n = vx_n1;
       pp = pp1;
     } else if (own && cells) {  // i == nx: the last x-faces are boundary faces
-      *reinterpret_cast<V*>(vx2 + i * ny + j0) = vx_i;
+      if (!FUSED || !h.nb_x[1]) *reinterpret_cast<V*>(vx2 + i * ny + j0) = vx_i;
     }
   }
+  // System-scope remote stores acknowledged before the wave retires (the sync
+  // kernel that publishes the arrival flags runs next on this stream).
+  if constexpr (FUSED) __builtin_amdgcn_s_waitcnt(0);
 }
 
 template <typename T>
@@ -296,10 +336,13 @@ void launch_acoustic2d(const AcousticArgs& a, hipStream_t stream) {
     const int64_t nseg = (a.ny + 1 + 62 * vj - 1) / (62 * vj), nch = (a.nx + 1 + ch - 1) / ch;
     const int64_t waves = nseg * nch;
     const dim3 grid(static_cast<unsigned>((waves + WAVES - 1) / WAVES));
+    const AcousticHalo none{};
     if (a.elem_bytes == 8)
-      hipLaunchKernelGGL((acoustic2d_vmarch_kernel<double, VJ8>), grid, dim3(64 * WAVES), 0, stream, a, ch);
+      hipLaunchKernelGGL((acoustic2d_vmarch_kernel<double, VJ8, false>), grid, dim3(64 * WAVES), 0, stream, a, ch,
+                         none);
     else
-      hipLaunchKernelGGL((acoustic2d_vmarch_kernel<float, VJ4>), grid, dim3(64 * WAVES), 0, stream, a, ch);
+      hipLaunchKernelGGL((acoustic2d_vmarch_kernel<float, VJ4, false>), grid, dim3(64 * WAVES), 0, stream, a, ch,
+                         none);
   } else if (g_acoustic_variant >= 1) {
     const int64_t ch = g_march_ch > 0 ? g_march_ch : MARCH_CH;
     const int64_t nseg = (a.ny + 1 + OWN - 1) / OWN, nch = (a.nx + 1 + ch - 1) / ch;
@@ -316,6 +359,22 @@ void launch_acoustic2d(const AcousticArgs& a, hipStream_t stream) {
     else
       hipLaunchKernelGGL(acoustic2d_kernel<float>, grid, dim3(BJ * BI), 0, stream, a);
   }
+  IGG_HIP_CHECK(hipGetLastError());
+}
+
+void launch_acoustic2d_fused(const AcousticArgs& a, const AcousticHalo& h, hipStream_t stream) {
+  if (a.elem_bytes != 4 && a.elem_bytes != 8)
+    fail("acoustic2d (fused halo): element size must be 4 or 8 bytes (got ", a.elem_bytes, ")");
+  const int vj = a.elem_bytes == 4 ? 4 : 2;
+  if (a.ny % vj != 0 || a.ny < 2 * vj || a.nx < 5 || a.ny < 5)
+    fail("acoustic2d (fused halo): needs ny % ", vj, " == 0 and nx, ny >= 5");
+  const int64_t ch = g_march_ch > 0 ? g_march_ch : VMARCH_CH;
+  const int64_t nseg = (a.ny + 1 + 62 * vj - 1) / (62 * vj), nch = (a.nx + 1 + ch - 1) / ch;
+  const dim3 grid(static_cast<unsigned>((nseg * nch + WAVES - 1) / WAVES));
+  if (a.elem_bytes == 8)
+    hipLaunchKernelGGL((acoustic2d_vmarch_kernel<double, 2, true>), grid, dim3(64 * WAVES), 0, stream, a, ch, h);
+  else
+    hipLaunchKernelGGL((acoustic2d_vmarch_kernel<float, 4, true>), grid, dim3(64 * WAVES), 0, stream, a, ch, h);
   IGG_HIP_CHECK(hipGetLastError());
 }
 

@@ -12,6 +12,14 @@ y-faces. One time step = ONE fused HIP kernel (csrc/kernels/acoustic_kernels.hip
 P2 everywhere, then Vx2/Vy2 on inner faces from P2 recomputed in registers)
 followed by ``update_halo_(Vx2, Vy2)`` (ol = 3 along the staggered dimension,
 2 along the other: mixed overlaps in one call) and a buffer swap.
+
+``set_fused(True)`` (GPU, a neighbour, overlap 2): the exchange moves into the
+sweep (csrc/include/igg/acoustic.hpp FusedAcoustic): the kernel stores the
+staggered boundary faces straight into the neighbours' next Vx2/Vy2 over xGMI
+and one 1-wave sync kernel completes the step; every other halo value is
+recomputed locally with the same arithmetic, so the fields are bitwise equal to
+the update_halo_ path (tests/test_acoustic.py) - the communication is hidden
+inside the HBM-bound sweep instead of following it.
 """
 from __future__ import annotations
 
@@ -52,13 +60,20 @@ class Acoustic2D:
         kw = dict(dtype=torch.float64, device=self.device)
         x = coords_g(0, self.dx, probe, **kw).view(-1, 1)
         y = coords_g(1, self.dy, probe, **kw).view(1, -1)
-        self.P = torch.exp(-((x - lx / 2) ** 2) - (y - ly / 2) ** 2).to(dtype).contiguous()
-        self.Vx = torch.zeros((nx + 1, ny), dtype=dtype, device=self.device)
-        self.Vy = torch.zeros((nx, ny + 1), dtype=dtype, device=self.device)
-        self.P2, self.Vx2, self.Vy2 = self.P.clone(), self.Vx.clone(), self.Vy.clone()
+        P = torch.exp(-((x - lx / 2) ** 2) - (y - ly / 2) ** 2).to(dtype).contiguous()
+        Vx = torch.zeros((nx + 1, ny), dtype=dtype, device=self.device)
+        Vy = torch.zeros((nx, ny + 1), dtype=dtype, device=self.device)
+        fields = [P, Vx, Vy, P.clone(), Vx.clone(), Vy.clone()]
+        if self.device.type == "cuda":
+            # One fine-grained allocation (the fused exchange stores into the
+            # neighbours' Vx2/Vy2 while their kernels run: docs/COHERENCE.md).
+            fields = _carve_fine(fields)
+        self.P, self.Vx, self.Vy, self.P2, self.Vx2, self.Vy2 = fields
         self.graph = None
         self.graph_steps = 2
         self._warm = False
+        self.fused = False
+        self._fa = None  # native FusedAcoustic (set_fused)
 
     def _update(self, P2, Vx2, Vy2, P, Vx, Vy) -> None:
         dev = self.device.type == "cuda"
@@ -67,9 +82,67 @@ class Acoustic2D:
                           self.nx, self.ny, self.dt * self.K, self.dt / self.rho, 1.0 / self.dx, 1.0 / self.dy,
                           P.element_size(), dev, s)
 
+    @property
+    def can_fuse(self) -> bool:
+        """Fused exchange possible: GPU, a neighbour in x or y, overlap 2 in
+        both, the vector kernel's shape (ny % 16 B-vector width, >= 5x5)."""
+        gg = _grid.global_grid()
+        if self.device.type != "cuda":
+            return False
+        if not any(int(gg.neighbors[s, d]) != -1 for s in range(2) for d in range(2)):
+            return False
+        if int(gg.overlaps[0]) != 2 or int(gg.overlaps[1]) != 2:
+            return False
+        vj = 4 if self.P.element_size() == 4 else 2
+        return self.ny % vj == 0 and self.nx >= 5 and self.ny >= 5
+
+    def set_fused(self, flag: bool) -> bool:
+        """Switch the fused halo exchange on/off (collective: every rank at the
+        same point; the first switch-on maps the neighbours' fields)."""
+        flag = bool(flag) and self.can_fuse
+        if flag == self.fused:
+            return flag
+        if flag and self._fa is None:
+            gg = _grid.global_grid()
+            nb = [[int(gg.neighbors[s, d]) for s in range(2)] for d in range(2)]
+            if gg.nprocs > 1:
+                mesh = native.PeerMesh(gg.comm.rank, gg.comm.size, gg.comm._allgather_bytes)
+            else:  # periodic / loopback single process: every neighbour is this rank
+                nb = [[0 if v >= 0 else -1 for v in row] for row in nb]
+                mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
+            self._fa = native.FusedAcoustic(mesh, self.nx, self.ny, self.P.element_size(), nb)
+            self._fa.set_fields(self.Vx.data_ptr(), self.Vx2.data_ptr(), self.Vy.data_ptr(), self.Vy2.data_ptr())
+        self.fused = flag
+        self.graph = None
+        return flag
+
+    def sync_halo(self) -> None:
+        """No-op: the fused step leaves every halo value as update_halo_ would
+        (the API matches Diffusion3D's, whose fused step defers halo planes)."""
+
+    def check(self) -> None:
+        """Raise if a fused-exchange sync kernel timed out waiting for a neighbour."""
+        if self._fa is not None:
+            self._fa.check_error()
+
+    def close(self) -> None:
+        """Release the fused exchange's peer mappings (collective: every rank)."""
+        if self._fa is not None:
+            torch.cuda.synchronize()
+            self._fa.close()
+            self._fa = None
+            self.fused = False
+            self.graph = None
+
     def step(self) -> None:
-        self._update(self.P2, self.Vx2, self.Vy2, self.P, self.Vx, self.Vy)
-        update_halo_(self.Vx2, self.Vy2)
+        if self.fused:
+            s = torch.cuda.current_stream().cuda_stream
+            self._fa.step(self.P2.data_ptr(), self.Vx2.data_ptr(), self.Vy2.data_ptr(), self.P.data_ptr(),
+                          self.Vx.data_ptr(), self.Vy.data_ptr(), self.nx, self.ny, self.dt * self.K,
+                          self.dt / self.rho, 1.0 / self.dx, 1.0 / self.dy, self.P.element_size(), s)
+        else:
+            self._update(self.P2, self.Vx2, self.Vy2, self.P, self.Vx, self.Vy)
+            update_halo_(self.Vx2, self.Vy2)
         self.P, self.P2 = self.P2, self.P
         self.Vx, self.Vx2 = self.Vx2, self.Vx
         self.Vy, self.Vy2 = self.Vy2, self.Vy
@@ -128,6 +201,25 @@ class Acoustic2D:
     def a_eff_bytes(self) -> int:
         """Each of P, Vx, Vy read once and written once per step."""
         return 2 * (self.P.numel() + self.Vx.numel() + self.Vy.numel()) * self.P.element_size()
+
+
+def _carve_fine(tensors):
+    """Copies of ``tensors`` carved from one native fine-grained allocation
+    (256 B-aligned slices)."""
+    from .diffusion3d import native_buffer
+
+    sizes = [t.numel() * t.element_size() for t in tensors]
+    offs, pos = [], 0
+    for n in sizes:
+        offs.append(pos)
+        pos += -(-n // 256) * 256
+    buf = native_buffer(pos, 1, tensors[0].device)
+    out = []
+    for t, o, n in zip(tensors, offs, sizes):
+        v = buf[o:o + n].view(t.dtype).view(t.shape)
+        v.copy_(t)
+        out.append(v)
+    return out
 
 
 def acoustic2d_reference(P, Vx, Vy, *, dt, K, rho, dx, dy):

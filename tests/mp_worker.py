@@ -215,6 +215,34 @@ def scenario_acoustic(dev, nx, ny, steps):
     print(f"rank {me} acoustic OK dims={dims.tolist()}")
 
 
+def scenario_acoustic_fused(dev, nx, ny, steps, periodic):
+    """Acoustic2D with the fused exchange vs the update_halo_ path, bitwise in
+    every field on every rank (eager steps, then hipGraph replays)."""
+    from igg.models.acoustic2d import Acoustic2D
+
+    _device(dev)
+    nx, ny, steps, per = int(nx), int(ny), int(steps), int(periodic)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, 1, periodx=per, periody=per, quiet=True,
+                                                          select_device=False, device_type="AMDGPU")
+    a, b = Acoustic2D(dtype=torch.float32), Acoustic2D(dtype=torch.float32)
+    assert b.set_fused(True), "fused exchange unavailable"
+    a.run(steps)
+    b.run(steps)
+    b.capture(steps=4)
+    a.run(8)
+    b.run(8)
+    torch.cuda.synchronize()
+    b.check()
+    for n in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2"):
+        x, y = getattr(a, n), getattr(b, n)
+        if not torch.equal(x, y):
+            bad = (x != y).nonzero()[:5].tolist()
+            raise AssertionError(f"rank {me} dims {dims.tolist()}: {n} differs at {bad}")
+    b.close()
+    igg.finalize_global_grid()
+    print(f"rank {me} acoustic fused OK dims={dims.tolist()}")
+
+
 def scenario_gather_async():
     """gather_async_: root pulls every block (IPC + copy engine), the caller
     overlaps other work, wait() reorders; then A may change again."""

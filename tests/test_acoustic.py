@@ -112,3 +112,71 @@ def test_gpu_vector_march_bitwise_equals_march(gpu, dtype, shape):
     eps = torch.finfo(dtype).eps
     for a, b in zip(*out):
         assert torch.allclose(a, b, rtol=8 * eps, atol=8 * eps)
+
+
+def _fused_pair(shape, periods, dtype, loopback=False):
+    from igg.parallel import halo as H
+
+    igg.init_global_grid(shape[0], shape[1], 1, periodx=periods[0], periody=periods[1], quiet=True, init_MPI=False)
+    if loopback:
+        H.enable_loopback((bool(periods[0]), bool(periods[1]), False))
+    a, b = Acoustic2D(dtype=dtype), Acoustic2D(dtype=dtype)
+    assert b.set_fused(True)
+    return a, b
+
+
+def _same(a, b):
+    return all(torch.equal(getattr(a, n), getattr(b, n)) for n in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("periods", [(1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("shape", [(64, 48), (37, 520), (9, 16)])
+def test_gpu_fused_matches_update_halo(gpu, dtype, periods, shape):
+    """Fused exchange (the kernel stores the staggered boundary faces into the
+    neighbours' next Vx2/Vy2; here the periodic neighbour is this rank) is
+    bitwise equal to kernel + update_halo_(Vx2, Vy2) in every field."""
+    a, b = _fused_pair(shape, periods, dtype)
+    a.run(9)
+    b.run(9)
+    torch.cuda.synchronize()
+    b.check()
+    assert _same(a, b)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_loopback_graph_and_switch(gpu):
+    """Loopback grid (every face through the remote path), hipGraph replays,
+    switching back to update_halo_ and on again."""
+    a, b = _fused_pair((66, 64), (1, 1), torch.float32, loopback=True)
+    a.run(3)
+    b.run(3)
+    b.capture(steps=4)
+    a.run(12)
+    b.run(12)
+    torch.cuda.synchronize()
+    b.check()
+    assert _same(a, b)
+    b.set_fused(False)
+    a.run(3)
+    b.run(3)
+    assert b.set_fused(True)
+    a.run(4)
+    b.run(4)
+    torch.cuda.synchronize()
+    assert _same(a, b)
+    b.close()
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,per", [(2, 1), (4, 0), (4, 1)])
+def test_gpu_fused_multirank(nprocs, per):
+    """Ranks sharing one GPU (put transport for the update_halo_ reference):
+    fused == update_halo_ bitwise on every rank, incl. graph replays."""
+    env = {"IGG_TRANSPORT": "put", "IGG_PUT_TIMEOUT": "20"}
+    if nprocs > 2:
+        env["GPU_MAX_HW_QUEUES"] = "1"
+    run_ranks(nprocs, "acoustic_fused", "gpu", 40, 36, 12, per, env_extra=env, timeout=150)
