@@ -374,6 +374,9 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
     else:
         t, gmode, sched = "host", None, "sequential"
     why = ""
+    if os.environ.get("IGG_BENCH_DEBUG_POST") and on_gpu and t == "put":  # diagnostics (collective)
+        eps = comm.all_gather_object(int(comm.mesh.epoch))
+        log(f"post-timing validation: put epochs per rank before the probe exchange: {eps}")
     try:
         if on_gpu and t != "put":
             H.set_halo_mode(sched)
@@ -394,6 +397,20 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
         if not torch.equal(X, R):
             bad = (X != R).nonzero()
             why = f"mismatch at {bad.shape[0]} entries, first {bad[0].tolist()}"
+        if os.environ.get("IGG_BENCH_DEBUG_POST") and on_gpu:  # which side is wrong (diagnostics; collective)
+            from igg.parallel.grid import global_grid
+
+            R2 = X0.clone()
+            H.update_halo_(R2)
+            _sync(comm)
+            H.set_transport(t)
+            X2 = X0.clone()
+            H.update_halo_(X2)
+            _sync(comm)
+            H.set_transport("staged")
+            print(f"rank {int(global_grid().me)}: ok {not why}; staged again == staged {torch.equal(R, R2)}, "
+                  f"put again == put {torch.equal(X, X2)}, put again == staged {torch.equal(X2, R)}; {why}",
+                  file=sys.stderr, flush=True)
     except Exception as e:  # a bounded wait expired, a transport error
         why = f"{type(e).__name__}: {e}"[:300]
         if getattr(comm, "mesh", None) is not None:

@@ -3,6 +3,7 @@
 // (src/update_halo.jl:32-78) would, with one sync kernel instead of
 // pack / send / unpack per dimension.
 #include <algorithm>
+#include <cstdlib>
 
 #include "igg/acoustic.hpp"
 #include "igg/common.hpp"
@@ -57,6 +58,11 @@ void FusedAcoustic::step(const AcousticArgs& a, hipStream_t stream) {
   // neighbour's output buffer k.
   const int64_t eb = elem_;
   AcousticHalo h;
+  static const int plain = [] {
+    const char* e = std::getenv("IGG_FUSED_PLAIN_STORES");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  h.plain_stores = plain;
   for (int s = 0; s < 2; ++s) {
     if (const int r = nb_[0][s]; r != PROC_NULL) {
       h.nb_x[s] = true;

@@ -47,6 +47,7 @@ struct AcousticHalo {
   uintptr_t send_x[2] = {0, 0};  // Vx2 rows (contiguous, pitch ny)
   uintptr_t send_y[2] = {0, 0};  // Vy2 columns (one element per row, pitch ny+1)
   bool nb_x[2] = {false, false}, nb_y[2] = {false, false};
+  int plain_stores = 0;  // debug (IGG_FUSED_PLAIN_STORES=1): plain instead of system-scope remote stores
 };
 
 void launch_acoustic2d(const AcousticArgs& a, hipStream_t stream);

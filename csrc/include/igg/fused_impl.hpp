@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "igg/stencil.hpp"
+#include "igg/sysstore.hpp"
 
 
 namespace igg {
@@ -86,38 +87,11 @@ struct HxScal {
   int peel;  // send mode bit 8: sweep the exchanged x planes of a chunk separately (kernel below)
 };
 
-// Writer side of the cross-device hand-off (docs/COHERENCE.md): every store
-// into peer memory (arena regions, or the neighbour's field with direct z) is
-// a system-scope store (sc0 sc1 = the encoding of a relaxed system-scope
-// atomic store on gfx942/gfx950): it writes through this XCD's L2, where the
-// peer mapping (MTYPE NC) could otherwise keep it dirty, and its vmcnt
-// acknowledgement means it reached the owner's memory. The wave ends with
-// s_waitcnt vmcnt(0) (hx_sweep), so when this kernel completes every peer
-// byte has landed; the sync kernel then publishes the flag. (A plain store +
-// per-wave buffer_wbl2 sc0 sc1 also works but writes back the XCD's whole
-// L2 from every storing wave: +14 % per step, profiles/r3_coherence/.)
-// Inline asm without a memory clobber: the destinations never alias anything
-// this kernel reads (restrict arguments), so the compiler may keep
-// scheduling loads across them; untracked by its vmcnt bookkeeping, the
-// stores only make its waits more conservative (in-order vmcnt on gfx9).
-template <typename V>
-__device__ __forceinline__ void st_sys(V* p, const V& v) {
-  static_assert(sizeof(V) == 4 || sizeof(V) == 8 || sizeof(V) == 16 || sizeof(V) == 32, "st_sys: 4..32 B");
-  if constexpr (sizeof(V) == 32) {
-    using H = unsigned __attribute__((ext_vector_type(4)));
-    struct P2 { H lo, hi; };
-    const P2 h = __builtin_bit_cast(P2, v);
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(h.lo));
-    asm volatile("global_store_dwordx4 %0, %1, off offset:16 sc0 sc1" ::"v"(p), "v"(h.hi));
-  } else if constexpr (sizeof(V) == 16) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
-  } else if constexpr (sizeof(V) == 8) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
-  } else {
-    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
-  }
-}
-
+// Writer side of the cross-device hand-off: every store into peer memory
+// (arena regions, or the neighbour's field with direct z) is a system-scope
+// store, st_sys (igg/sysstore.hpp). (A plain store + per-wave buffer_wbl2
+// sc0 sc1 also works but writes back the XCD's whole L2 from every storing
+// wave: +14 % per step, profiles/r3_coherence/.)
 
 // FEAT bits (compile-time exchange features): 1 x-in, 2 y-in, 4 z-in, 8 z-out,
 // 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants); 512 =

@@ -73,6 +73,7 @@ class PeerMesh {
   uint64_t* flags_ = nullptr;
   char* arena_ = nullptr;
   size_t arena_bytes_ = 0;
+  std::vector<char*> retired_;  // grown-out arenas, freed at close() (never re-exported addresses)
   std::vector<uint64_t*> peer_flags_;
   std::vector<char*> peer_arena_;
   std::vector<void*> mapped_;  // map_buffers() mappings (one per distinct peer allocation)

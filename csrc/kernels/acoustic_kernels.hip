@@ -11,6 +11,7 @@
 #include "igg/acoustic.hpp"
 #include "igg/common.hpp"
 #include "igg/copy.hpp"
+#include "igg/sysstore.hpp"
 
 namespace igg {
 namespace {
@@ -152,24 +153,27 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_march_kernel(AcousticAr
 // the neighbours inside this sweep. Row i = 2 of Vx2 goes to the x-low
 // neighbour's row nx, row nx-2 to the x-high neighbour's row 0; column 2 of
 // Vy2 to the y-low neighbour's column ny, column ny-2 to the y-high
-// neighbour's column 0 - system-scope stores (st_sys: written through this
-// XCD's L2, acknowledged by the owner's memory before the wave retires); and
+// neighbour's column 0 - system-scope stores (st_sys, igg/sysstore.hpp:
+// written through this XCD's L2, acknowledged by the owner's memory before
+// the wave retires); and
 // this rank's own faces on a side with a neighbour are not written here (the
 // neighbour stores them).
 template <typename T>
-__device__ __forceinline__ void st_sys(T* p, const T& v) {
-  static_assert(sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16, "st_sys: 4, 8 or 16 B");
-  if constexpr (sizeof(T) == 16)
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
-  else if constexpr (sizeof(T) == 8)
-    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
-  else
-    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
+__device__ __forceinline__ void st_remote(T* p, const T& v, int plain) {
+  if (plain) *p = v;  // debug knob (IGG_FUSED_PLAIN_STORES=1), single device only
+  else st_sys(p, v);
 }
 
 template <typename T, int VJ, bool FUSED>
 __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticArgs a, int64_t ch,
                                                                      AcousticHalo h) {
+  // No FMA contraction: every value is rounded per operation, so a point gets
+  // bitwise the same result wherever it is computed - in the march loop or in
+  // a chunk's first-row recomputation of P2(i-1), on this rank or on the
+  // neighbour that owns it (the fused exchange recomputes halo values locally
+  // instead of receiving them: acoustic.hpp FusedAcoustic). Memory-bound
+  // kernel: the extra VALU operations are free.
+#pragma clang fp contract(off)
   typedef T V __attribute__((ext_vector_type(VJ)));
   typedef T VU __attribute__((ext_vector_type(VJ), aligned(sizeof(T))));
   constexpr int64_t OWNV = 62 * VJ;
@@ -253,8 +257,8 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
           if constexpr (FUSED) {
             // face 0 of a side with a neighbour: the neighbour stores it
             if (!(i == 0 && h.nb_x[0])) __builtin_nontemporal_store(vxo, reinterpret_cast<V*>(vx2 + i * ny + j0));
-            if (i == 2 && h.send_x[0]) st_sys(reinterpret_cast<V*>(h.send_x[0]) + j0 / VJ, vxo);
-            if (i == nx - 2 && h.send_x[1]) st_sys(reinterpret_cast<V*>(h.send_x[1]) + j0 / VJ, vxo);
+            if (i == 2 && h.send_x[0]) st_remote(reinterpret_cast<V*>(h.send_x[0]) + j0 / VJ, vxo, h.plain_stores);
+            if (i == nx - 2 && h.send_x[1]) st_remote(reinterpret_cast<V*>(h.send_x[1]) + j0 / VJ, vxo, h.plain_stores);
             if (j0 == 0 && h.nb_y[0]) {  // column 0 is the y-low neighbour's to store
 #pragma unroll
               for (int e = 1; e < VJ; ++e) vy2[i * sy + e] = vyo[e];
@@ -262,8 +266,8 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
               *reinterpret_cast<VU*>(vy2 + i * sy + j0) = vyo;
             }
             const int64_t r2 = 2 - j0, rn = ny - 2 - j0;  // element of column 2 / ny-2 in this lane
-            if (h.send_y[0] && r2 >= 0 && r2 < VJ) st_sys(reinterpret_cast<T*>(h.send_y[0]) + i * sy, vyo[r2]);
-            if (h.send_y[1] && rn >= 0 && rn < VJ) st_sys(reinterpret_cast<T*>(h.send_y[1]) + i * sy, vyo[rn]);
+            if (h.send_y[0] && r2 >= 0 && r2 < VJ) st_remote(reinterpret_cast<T*>(h.send_y[0]) + i * sy, vyo[r2], h.plain_stores);
+            if (h.send_y[1] && rn >= 0 && rn < VJ) st_remote(reinterpret_cast<T*>(h.send_y[1]) + i * sy, vyo[rn], h.plain_stores);
           } else {
             __builtin_nontemporal_store(vxo, reinterpret_cast<V*>(vx2 + i * ny + j0));
             *reinterpret_cast<VU*>(vy2 + i * sy + j0) = vyo;

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "igg/copy.hpp"
+#include "igg/sysstore.hpp"
 
 namespace igg {
 namespace {
@@ -30,22 +31,11 @@ __device__ __forceinline__ int64_t parity_shift(const CopyBatch& b) {
 }
 
 // Element store: plain, or (SYS, put transport) a system-scope store
-// (sc0 sc1, the encoding of a relaxed system-scope atomic store on gfx950).
+// (st_sys, igg/sysstore.hpp).
 template <typename T, bool SYS>
 __device__ __forceinline__ void store(T* p, const T& v) {
-  if constexpr (!SYS) {
-    *p = v;
-  } else if constexpr (sizeof(T) == 16) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v)));
-  } else if constexpr (sizeof(T) == 8) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
-  } else if constexpr (sizeof(T) == 4) {
-    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v));
-  } else if constexpr (sizeof(T) == 2) {
-    asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p), "v"(static_cast<unsigned>(v)));
-  } else {
-    asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p), "v"(static_cast<unsigned>(v)));
-  }
+  if constexpr (SYS) st_sys(p, v);
+  else *p = v;
 }
 
 template <typename T, bool FENCE>

@@ -5,6 +5,7 @@
 
 #include "igg/ipc.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <ios>
@@ -24,6 +25,10 @@ PeerMesh::PeerMesh(int rank, int nranks, AllGather allgather)
   timeout_ticks_ = put_timeout_ticks(seconds);
   if (const char* k = std::getenv("IGG_PUT_ARENA_KIND")) arena_kind_ = static_cast<MemKind>(std::atoi(k));
   exchange_handles(true);
+  if (const char* m = std::getenv("IGG_PUT_ARENA_MIN")) {
+    const long long mb = std::atoll(m);
+    if (mb > 0) ensure_arena(static_cast<size_t>(mb) << 20);  // collective
+  }
 }
 
 uint64_t PeerMesh::read_flag(int idx) const {
@@ -62,6 +67,7 @@ PeerMesh::~PeerMesh() {
   for (void* p : mapped_) (void)hipIpcCloseMemHandle(p);
   mapped_.clear();
   if (arena_) (void)hipFree(arena_);
+  for (char* a : retired_) (void)hipFree(a);
   if (flags_) (void)hipFree(flags_);
   if (side_) (void)hipStreamDestroy(side_);
   arena_ = nullptr;
@@ -103,9 +109,16 @@ void PeerMesh::exchange_handles(bool flags_too) {
 void PeerMesh::ensure_arena(size_t bytes) {
   if (closed_) fail("PeerMesh: used after close()");
   if (bytes <= arena_bytes_) return;
-  bytes = static_cast<size_t>(round_up(static_cast<int64_t>(bytes), 1 << 20));
+  // Geometric growth with a floor: a regrowth is a collective re-export, so
+  // make it rare (one field of 1024^3 f32 needs 2 x 24 MiB).
+  static const size_t floor_bytes = [] {
+    const char* f = std::getenv("IGG_PUT_ARENA_FLOOR_MB");  // tests lower it to exercise regrowth
+    const long long mb = f ? std::atoll(f) : 64;
+    return static_cast<size_t>(mb > 0 ? mb : 1) << 20;
+  }();
+  bytes = static_cast<size_t>(round_up(static_cast<int64_t>(std::max({bytes, 2 * arena_bytes_, floor_bytes})), 1 << 20));
   // Every rank drains its own puts/unpacks into the old arenas, then agrees
-  // (allgather = barrier) before anyone unmaps or frees them.
+  // (allgather = barrier) before anyone unmaps them.
   IGG_HIP_CHECK(hipDeviceSynchronize());
   (void)allgather_(std::string());
   for (int r = 0; r < nranks_; ++r)
@@ -114,7 +127,13 @@ void PeerMesh::ensure_arena(size_t bytes) {
       peer_arena_[r] = nullptr;
     }
   (void)allgather_(std::string());
-  if (arena_) ipc_free(arena_);
+  // The old arena is retired, not freed, until close(): a freed allocation's
+  // address can come back for the new one, and an IPC export of an allocation
+  // at a reused address was observed to map the OLD memory in the peers
+  // (every message of that sender lost, deterministically for the rest of the
+  // run; also hipIpcGetMemHandle 'invalid argument') on MI355X / ROCm 7.2
+  // (profiles/r3_put_arena/). Keeping it alive makes every export address new.
+  if (arena_) retired_.push_back(arena_);
   arena_ = static_cast<char*>(ipc_malloc(bytes, arena_kind_));
   arena_bytes_ = bytes;
   exchange_handles(false);
@@ -210,6 +229,8 @@ void PeerMesh::close() {
   }
   (void)allgather_(std::string());
   if (arena_) ipc_free(arena_);
+  for (char* a : retired_) ipc_free(a);
+  retired_.clear();
   if (flags_) ipc_free(flags_);
   arena_ = nullptr;
   flags_ = nullptr;

@@ -64,11 +64,20 @@ class Acoustic2D:
         Vx = torch.zeros((nx + 1, ny), dtype=dtype, device=self.device)
         Vy = torch.zeros((nx, ny + 1), dtype=dtype, device=self.device)
         fields = [P, Vx, Vy, P.clone(), Vx.clone(), Vy.clone()]
-        if self.device.type == "cuda":
+        import os as _os
+
+        if self.device.type == "cuda" and _os.environ.get("IGG_FIELD_MEMORY", "fine") != "torch":
             # One fine-grained allocation (the fused exchange stores into the
             # neighbours' Vx2/Vy2 while their kernels run: docs/COHERENCE.md).
             fields = _carve_fine(fields)
         self.P, self.Vx, self.Vy, self.P2, self.Vx2, self.Vy2 = fields
+        # P's halo cells, evaluated from the global coordinates above, equal
+        # the neighbours' cells only up to rounding (periodic wrap of x_g);
+        # one exchange makes them bitwise consistent, so every halo value the
+        # step recomputes locally equals what update_halo_ would deliver (the
+        # fused exchange relies on it: set_fused). P itself is never exchanged
+        # again: P2 is recomputed everywhere from halo-consistent inputs.
+        update_halo_(self.P)
         self.graph = None
         self.graph_steps = 2
         self._warm = False

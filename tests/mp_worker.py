@@ -243,6 +243,117 @@ def scenario_acoustic_fused(dev, nx, ny, steps, periodic):
     print(f"rank {me} acoustic fused OK dims={dims.tolist()}")
 
 
+def scenario_put_after_model(n, graph, steps):
+    """Put transport: the acoustic model's (Vx2, Vy2) exchanges (eager, then
+    hipGraph replays if ``graph``), then a single-field probe exchange, bitwise
+    against the host-staged path on every rank (bench.py's post-timing
+    validation in miniature); prints the put epoch of every rank."""
+    from igg.models.acoustic2d import Acoustic2D
+    from igg.parallel import halo as H
+
+    _device("gpu")
+    n, graph, steps = int(n), int(graph), int(steps)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, 1, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    gg = igg.get_global_grid()
+    m = Acoustic2D(dtype=torch.float32)
+    H.set_transport("put")
+    m.run(3)
+    if graph:
+        m.capture(steps=4)
+    m.run(steps)
+    torch.cuda.synchronize()
+    A = torch.zeros(n, n, dtype=torch.float32)
+    encode(A)
+    ref = expected_after_halo(A, has_halo(A, gg), gg.neighbors.tolist())
+    X = zero_boundaries(A.clone()).cuda()
+    igg.update_halo_(X)
+    torch.cuda.synchronize()
+    ep = comm.mesh.epoch
+    got = X.cpu()
+    bad = (got != ref).nonzero()
+    print(f"rank {me} epoch {ep} mismatches {bad.shape[0]} first {bad[:6].tolist()}", flush=True)
+    eps = comm.all_gather_object(int(ep))
+    assert len(set(eps)) == 1, f"put epochs differ across ranks: {eps}"
+    assert bad.shape[0] == 0, f"rank {me}: probe mismatch at {bad[:6].tolist()}"
+    igg.finalize_global_grid()
+    print(f"rank {me} put after model OK", flush=True)
+
+
+def scenario_put_regrow():
+    """Put transport with field sets that force the receive arenas to grow
+    (a collective re-export of IPC memory) several times (growth floor
+    lowered by IGG_PUT_ARENA_FLOOR_MB), each exchange checked against the
+    halo oracle; then small field sets again (profiles/r3_put_arena/: an
+    export at a reused address mapped stale memory in the peers)."""
+    _device("gpu")
+    n = 40
+    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n, n, periodx=1, periody=1, periodz=1, quiet=True,
+                                                          select_device=False, device_type="AMDGPU")
+    gg = igg.get_global_grid()
+    from igg.parallel import halo as H
+
+    H.set_transport("put")
+    sizes = []
+    for k in (1, 3, 8, 20, 1, 5, 40, 2):
+        fs, refs = [], []
+        for i in range(k):
+            A = torch.zeros(n, n, n, dtype=torch.float64)
+            encode(A)
+            A += 1000 * i
+            refs.append(expected_after_halo(A, has_halo(A, gg), gg.neighbors.tolist()))
+            fs.append(zero_boundaries(A.clone()).cuda())
+        igg.update_halo_(*fs)
+        igg.update_halo_(*fs)  # both arena halves
+        for i, (X, R) in enumerate(zip(fs, refs)):
+            got = X.cpu()
+            assert torch.equal(got, R), f"rank {me} k={k} field {i}: mismatch at {(got != R).nonzero()[:5].tolist()}"
+        sizes.append(gg.comm.mesh.arena_bytes >> 10)
+        print(f"rank {me} k={k} arena {sizes[-1]} KiB OK", flush=True)
+    assert len(set(sizes)) >= 3, f"the arena did not regrow: {sizes}"
+    igg.finalize_global_grid()
+    print(f"rank {me} put regrow OK", flush=True)
+
+
+def scenario_acoustic_fused_soak(nx, ny, steps, periodic, graph):
+    """Long fused acoustic run vs the update_halo_ path (put transport), compared
+    after every step (eager) or every 4 (graph replays): reports the first
+    diverging step, field and position on this rank."""
+    from igg.models.acoustic2d import Acoustic2D
+
+    _device("gpu")
+    nx, ny, steps, per, graph = int(nx), int(ny), int(steps), int(periodic), int(graph)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, 1, periodx=per, periody=per, quiet=True,
+                                                          select_device=False, device_type="AMDGPU")
+    from igg.parallel import halo as H
+
+    H.set_transport("put")
+    a, b = Acoustic2D(dtype=torch.float32), Acoustic2D(dtype=torch.float32)
+    assert b.set_fused(True)
+    if graph:
+        a.capture(steps=4)
+        b.capture(steps=4)
+    k = 4 if graph else 1
+    first = None
+    for s in range(0, steps, k):
+        a.run(k)
+        b.run(k)
+        torch.cuda.synchronize()
+        if first is None:
+            for n in ("P", "Vx", "Vy"):
+                x, y = getattr(a, n), getattr(b, n)
+                if not torch.equal(x, y):
+                    first = (s + k, n, (x != y).nonzero()[:4].tolist(), int((x != y).sum()))
+                    break
+    b.check()
+    print(f"rank {me} coords {coords.tolist()} first divergence: {first}", flush=True)
+    flag = comm.all_gather_object(first is None)
+    b.close()
+    igg.finalize_global_grid()
+    assert all(flag), f"rank {me}: diverged {first}"
+    print(f"rank {me} acoustic fused soak OK", flush=True)
+
+
 def scenario_gather_async():
     """gather_async_: root pulls every block (IPC + copy engine), the caller
     overlaps other work, wait() reorders; then A may change again."""

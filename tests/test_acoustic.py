@@ -126,7 +126,15 @@ def _fused_pair(shape, periods, dtype, loopback=False):
 
 
 def _same(a, b):
-    return all(torch.equal(getattr(a, n), getattr(b, n)) for n in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2"))
+    bad = []
+    for n in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2"):
+        x, y = getattr(a, n), getattr(b, n)
+        if not torch.equal(x, y):
+            d = (x != y).nonzero()
+            bad.append(f"{n}: {d.shape[0]} entries, first {d[:4].tolist()}, max |diff| "
+                       f"{(x.double() - y.double()).abs().max().item():.3e}")
+    assert not bad, "; ".join(bad)
+    return True
 
 
 @pytest.mark.gpu

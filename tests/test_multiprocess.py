@@ -97,6 +97,14 @@ def test_put_transport_timeout_reports_and_never_hangs():
 
 
 @pytest.mark.gpu
+def test_put_transport_arena_regrowth():
+    """Receive arenas that grow several times (collective re-export of IPC
+    memory) keep every exchange exact on 4 ranks."""
+    run_ranks(4, "put_regrow", env_extra={"IGG_TRANSPORT": "staged", "IGG_PUT_TIMEOUT": "20",
+                                          "IGG_PUT_ARENA_FLOOR_MB": "1", "GPU_MAX_HW_QUEUES": "1"}, timeout=150)
+
+
+@pytest.mark.gpu
 def test_put_transport_absorbs_rank_skew():
     run_ranks(4, "put_skew", 12, env_extra=PUT_ENV, timeout=170)
 
