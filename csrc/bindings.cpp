@@ -555,14 +555,14 @@ PYBIND11_MODULE(_igg_native, m) {
       .def("step",
            [](FusedAcoustic& f, uintptr_t p2, uintptr_t vx2, uintptr_t vy2, uintptr_t p, uintptr_t vx, uintptr_t vy,
               int64_t nx, int64_t ny, double dtk, double dt_rho, double rdx, double rdy, int elem_bytes,
-              uintptr_t stream) {
+              uintptr_t stream, bool entry) {
              TraceRange tr("igg.acoustic2d_fused");
              AcousticArgs a{p2, vx2, vy2, p, vx, vy, nx, ny, dtk, dt_rho, rdx, rdy, elem_bytes};
-             f.step(a, as_stream(stream));
+             f.step(a, as_stream(stream), entry);
            },
            py::arg("p2"), py::arg("vx2"), py::arg("vy2"), py::arg("p"), py::arg("vx"), py::arg("vy"), py::arg("nx"),
            py::arg("ny"), py::arg("dtk"), py::arg("dt_rho"), py::arg("rdx"), py::arg("rdy"), py::arg("elem_bytes"),
-           py::arg("stream"))
+           py::arg("stream"), py::arg("entry") = false)
       .def("check_error", &FusedAcoustic::check_error)
       .def("close", &FusedAcoustic::close);
   m.def("acoustic2d_set_variant", &acoustic2d_set_variant);
@@ -618,14 +618,16 @@ PYBIND11_MODULE(_igg_native, m) {
            py::arg("mesh"), py::arg("n"), py::arg("elem_bytes"), py::arg("neighbors"))
       .def("step",
            [](FusedHalo& f, uintptr_t t2, uintptr_t t, uintptr_t cp, const std::array<double, 3>& rd2,
-              double dtlam, int variant, int64_t step, bool primed, uintptr_t stream, int rounds, int mode) {
+              double dtlam, int variant, int64_t step, bool primed, uintptr_t stream, int rounds, int mode,
+              bool entry) {
              TraceRange tr("igg.diffusion3d_fused");
              DiffusionArgs a{t2, t, cp, {0, 0, 0}, {rd2[0], rd2[1], rd2[2]}, dtlam, 0, rounds};
              f.step_shape(a);
-             f.step(a, variant, mode, step, primed, as_stream(stream));
+             f.step(a, variant, mode, step, primed, as_stream(stream), entry);
            },
            py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("rd2"), py::arg("dtlam"), py::arg("variant"),
-           py::arg("step"), py::arg("primed"), py::arg("stream"), py::arg("rounds") = 0, py::arg("mode") = 0)
+           py::arg("step"), py::arg("primed"), py::arg("stream"), py::arg("rounds") = 0, py::arg("mode") = 0,
+           py::arg("entry") = false)
       .def("sync", [](FusedHalo& f, uintptr_t s) { f.sync(as_stream(s)); })
       .def("set_fields", &FusedHalo::set_fields, py::arg("a"), py::arg("b"))
       .def_property_readonly("has_fields", &FusedHalo::has_fields)

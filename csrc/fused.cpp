@@ -97,10 +97,11 @@ HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z)
 }
 
 void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed,
-                     hipStream_t stream) {
+                     hipStream_t stream, bool entry) {
   for (int d = 0; d < 3; ++d)
     if (a.n[d] != n_[d]) fail("FusedHalo.step: field shape does not match the fused halo's local grid");
   if (a.elem_bytes != elem_) fail("FusedHalo.step: field dtype does not match the fused halo");
+  if (entry) sync(stream);  // entry barrier (fused.hpp)
   launch_diffusion3d_fused(a, io(step, primed, a.t2, (mode & 4) != 0), variant, mode, stream);
   sync(stream);
 }

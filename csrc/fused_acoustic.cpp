@@ -45,7 +45,7 @@ void FusedAcoustic::set_fields(uintptr_t vx_a, uintptr_t vx_b, uintptr_t vy_a, u
   fields_ = mesh_->map_buffers({vx_a, vx_b, vy_a, vy_b});  // collective
 }
 
-void FusedAcoustic::step(const AcousticArgs& a, hipStream_t stream) {
+void FusedAcoustic::step(const AcousticArgs& a, hipStream_t stream, bool entry) {
   if (fields_.empty()) fail("FusedAcoustic.step: set_fields first");
   if (a.nx != nx_ || a.ny != ny_ || a.elem_bytes != elem_)
     fail("FusedAcoustic.step: fields do not match the fused exchange's local grid");
@@ -75,6 +75,7 @@ void FusedAcoustic::step(const AcousticArgs& a, hipStream_t stream) {
       h.send_y[s] = reinterpret_cast<uintptr_t>(fields_.at(r)[2 + k] + (s == 0 ? ny_ : 0) * eb);
     }
   }
+  if (entry) launch_put_sync(sync_, stream);  // entry barrier
   launch_acoustic2d_fused(a, h, stream);
   launch_put_sync(sync_, stream);
 }

@@ -82,7 +82,9 @@ class FusedAcoustic {
                 const std::array<std::array<int, 2>, 2>& nb);
   // Collective: the ping-pong buffers of Vx and Vy (same order on every rank).
   void set_fields(uintptr_t vx_a, uintptr_t vx_b, uintptr_t vy_a, uintptr_t vy_b);
-  void step(const AcousticArgs& a, hipStream_t stream);
+  // `entry`: a sync kernel first (a neighbour's remote stores must not
+  // overtake this rank's own earlier writes to the fields: FusedHalo::step).
+  void step(const AcousticArgs& a, hipStream_t stream, bool entry = false);
   void check_error() const;
   void close();
 

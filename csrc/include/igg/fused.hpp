@@ -65,8 +65,12 @@ class FusedHalo {
   // neighbour's t2 is its buffer k".
   void set_fields(uintptr_t a, uintptr_t b);
   bool has_fields() const { return !fields_.empty(); }
-  // Stencil with fused send/receive + sync kernel, on `stream`.
-  void step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed, hipStream_t stream);
+  // Stencil with fused send/receive + sync kernel, on `stream`. `entry`: a
+  // sync kernel first - the neighbours' remote stores of this step must not
+  // overtake this rank's own earlier writes to the fields or the arena (a
+  // restore, a switch into fused mode); every rank passes the same flag.
+  void step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed, hipStream_t stream,
+            bool entry = false);
   // Fill the shape/dtype of `a` from this halo's local grid.
   void step_shape(DiffusionArgs& a) const {
     for (int d = 0; d < 3; ++d) a.n[d] = n_[d];

@@ -83,6 +83,10 @@ class Acoustic2D:
         self._warm = False
         self.fused = False
         self._fa = None  # native FusedAcoustic (set_fused)
+        # The next fused step starts with an entry barrier: the neighbours'
+        # remote stores must not overtake this rank's own writes to the fields
+        # (switch into fused mode, restore, external edits: mark_modified).
+        self._entry = True
 
     def _update(self, P2, Vx2, Vy2, P, Vx, Vy) -> None:
         dev = self.device.type == "cuda"
@@ -122,8 +126,16 @@ class Acoustic2D:
             self._fa = native.FusedAcoustic(mesh, self.nx, self.ny, self.P.element_size(), nb)
             self._fa.set_fields(self.Vx.data_ptr(), self.Vx2.data_ptr(), self.Vy.data_ptr(), self.Vy2.data_ptr())
         self.fused = flag
+        self._entry = True
         self.graph = None
         return flag
+
+    def mark_modified(self) -> None:
+        """Declare that the fields were written outside the time loop (e.g. a
+        copy into P/Vx/Vy): the next fused step first synchronises with the
+        neighbours, which store into this rank's fields (collective: every rank
+        calls it at the same point)."""
+        self._entry = True
 
     def sync_halo(self) -> None:
         """No-op: the fused step leaves every halo value as update_halo_ would
@@ -148,7 +160,9 @@ class Acoustic2D:
             s = torch.cuda.current_stream().cuda_stream
             self._fa.step(self.P2.data_ptr(), self.Vx2.data_ptr(), self.Vy2.data_ptr(), self.P.data_ptr(),
                           self.Vx.data_ptr(), self.Vy.data_ptr(), self.nx, self.ny, self.dt * self.K,
-                          self.dt / self.rho, 1.0 / self.dx, 1.0 / self.dy, self.P.element_size(), s)
+                          self.dt / self.rho, 1.0 / self.dx, 1.0 / self.dy, self.P.element_size(), s,
+                          self._entry)
+            self._entry = False
         else:
             self._update(self.P2, self.Vx2, self.Vy2, self.P, self.Vx, self.Vy)
             update_halo_(self.Vx2, self.Vy2)
@@ -165,8 +179,8 @@ class Acoustic2D:
             raise RuntimeError("Acoustic2D.capture: hipGraphs need a GPU model")
         if steps < 2 or steps % 2:
             raise ValueError("Acoustic2D.capture: steps must be even and >= 2")
-        if not self._warm:
-            self.step()
+        if not self._warm or (self.fused and self._entry):
+            self.step()  # the graph holds steady-state steps only (no entry barrier)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
@@ -204,6 +218,7 @@ class Acoustic2D:
                 raise ValueError(f"Acoustic2D.restore: {name} is {tuple(f[name].shape)}/{f[name].dtype}, "
                                  f"the model has {tuple(dst.shape)}/{dst.dtype}")
             dst.copy_(f[name])
+        self._entry = True
         return int(meta["step"])
 
     @property

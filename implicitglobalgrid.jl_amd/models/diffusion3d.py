@@ -161,6 +161,11 @@ class Diffusion3D:
         self._fh = None
         self._fstep = 0
         self._fprimed = False
+        # Entry barrier before the next fused step (neighbours store into this
+        # rank's arena and, with direct z, its fields: their stores must not
+        # overtake this rank's own earlier writes - a switch into fused mode, a
+        # restore, external edits: mark_modified).
+        self._fentry = True
         self._graph_fused = None  # fused mode / step parity the graph was captured with
         self._graph_parity = 0
 
@@ -199,6 +204,7 @@ class Diffusion3D:
                 self.fused_variant = 0
             self.set_overlap(False)
             self._fprimed = False  # the field's halo planes are valid right now
+            self._fentry = True
         else:
             self.sync_halo()
         self.fused = flag
@@ -211,6 +217,13 @@ class Diffusion3D:
         if self.fused and self._fprimed:
             update_halo_(self.T)
             self._fprimed = False
+
+    def mark_modified(self) -> None:
+        """Declare that T/T2 were written outside the time loop: the next fused
+        step first synchronises with the neighbours (collective) and reads its
+        halos from T."""
+        self._fprimed = False
+        self._fentry = True
 
     def close(self) -> None:
         """Release the fused exchange's peer mesh (collective: every rank)."""
@@ -245,6 +258,7 @@ class Diffusion3D:
                                  f"the model has {tuple(dst.shape)}/{dst.dtype}")
             dst.copy_(f[name])
         self._fprimed = False  # the fused arena does not hold these halos; T's own halo planes do
+        self._fentry = True
         return int(meta["step"])
 
     def check(self) -> None:
@@ -284,11 +298,12 @@ class Diffusion3D:
                 with self.timer.phase("stencil+exchange"):
                     self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
                                   self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
-                                  self.fused_mode)
+                                  self.fused_mode, self._fentry)
             else:
                 self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
                               self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
-                              self.fused_mode)
+                              self.fused_mode, self._fentry)
+            self._fentry = False
             self._fstep += 1
             self._fprimed = True
         elif self.overlap:
