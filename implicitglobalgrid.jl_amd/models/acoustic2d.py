@@ -80,6 +80,7 @@ class Acoustic2D:
         update_halo_(self.P)
         self.graph = None
         self.graph_steps = 2
+        self._graph_P = 0  # P's buffer when the graph was captured
         self._warm = False
         self.fused = False
         self._fa = None  # native FusedAcoustic (set_fused)
@@ -190,14 +191,24 @@ class Acoustic2D:
         register_graph(g)
         self.graph = g
         self.graph_steps = steps
+        self._graph_P = self.P.data_ptr()
 
     def run(self, nt: int) -> None:
         if self.graph is not None:
+            # The captured steps read the capture's P/Vx/Vy first and hold no
+            # entry barrier: one eager step realigns an odd step count or
+            # performs a pending barrier (mark_modified, restore).
+            while nt > 0 and not self._graph_ready():
+                self.step()
+                nt -= 1
             for _ in range(nt // self.graph_steps):
                 self.graph.replay()
             nt %= self.graph_steps
         for _ in range(nt):
             self.step()
+
+    def _graph_ready(self) -> bool:
+        return self.P.data_ptr() == self._graph_P and not (self.fused and self._entry)
 
     def save(self, prefix: str, step: int = 0) -> str:
         """Per-rank checkpoint of the model state (collective; utils.checkpoint)."""

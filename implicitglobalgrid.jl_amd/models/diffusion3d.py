@@ -168,6 +168,7 @@ class Diffusion3D:
         self._fentry = True
         self._graph_fused = None  # fused mode / step parity the graph was captured with
         self._graph_parity = 0
+        self._graph_T = 0  # T's buffer when the graph was captured
 
     @property
     def can_fuse(self) -> bool:
@@ -384,23 +385,38 @@ class Diffusion3D:
         self.graph_steps = steps
         self._graph_fused = self.fused
         self._graph_parity = self._fstep % 2
+        self._graph_T = self.T.data_ptr()
 
     def run(self, nt: int) -> None:
         """Advance ``nt`` steps (by graph replays of ``graph_steps`` steps if captured)."""
         if self.graph is not None and self._graph_fused == self.fused:
-            # The captured fused steps have their arena halves baked in: they
-            # assume a primed arena and the step-counter parity of the capture.
-            while self.fused and nt > 0 and (self._fstep % 2 != self._graph_parity or not self._fprimed):
+            # The captured steps have their buffer roles baked in (T of the
+            # capture is read first) and, fused, their arena halves too: they
+            # assume a primed arena, no pending entry barrier and the
+            # step-counter parity of the capture. Eager steps realign (at most
+            # two; a mode switch between captures can make the two parities
+            # disagree for good: then the rest runs eagerly).
+            for _ in range(2):
+                if nt == 0 or self._graph_ready():
+                    break
                 self.step()
                 nt -= 1
-            k = self.graph_steps
-            for _ in range(nt // k):
-                self.graph.replay()
-            if self.fused:
-                self._fstep += k * (nt // k)
-            nt %= k
+            if self._graph_ready():
+                k = self.graph_steps
+                for _ in range(nt // k):
+                    self.graph.replay()
+                if self.fused:
+                    self._fstep += k * (nt // k)
+                nt %= k
         for _ in range(nt):
             self.step()
+
+    def _graph_ready(self) -> bool:
+        if self.T.data_ptr() != self._graph_T:
+            return False
+        if self.fused:
+            return self._fstep % 2 == self._graph_parity and self._fprimed and not self._fentry
+        return True
 
     @property
     def a_eff_bytes(self) -> int:

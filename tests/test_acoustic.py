@@ -95,6 +95,34 @@ def test_gpu_model_graph_matches_eager(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
+def test_gpu_graph_after_odd_step_counts(gpu, fused):
+    """run() after an odd number of steps (and after a restore-like write with
+    mark_modified) realigns the buffer roles the graph was captured with."""
+    igg.init_global_grid(64, 48, 1, periodx=1, periody=1, quiet=True, init_MPI=False)
+    a, b = Acoustic2D(dtype=torch.float32), Acoustic2D(dtype=torch.float32)
+    if fused:
+        assert b.set_fused(True)
+    b.capture(steps=4)
+    a.run(1)  # capture ran one eager step
+    for k in (5, 3, 8, 7):
+        a.run(k)
+        b.run(k)
+    saved = {n: getattr(a, n).clone() for n in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2")}
+    for m in (a, b):
+        for n, t in saved.items():
+            getattr(m, n).copy_(t)
+    b.mark_modified()
+    a.run(9)
+    b.run(9)
+    torch.cuda.synchronize()
+    b.check()
+    assert _same(a, b)
+    b.close()
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("shape", [(300, 1024), (64, 520), (9, 16)])
 def test_gpu_vector_march_bitwise_equals_march(gpu, dtype, shape):

@@ -132,7 +132,7 @@ def test_share_gpu_post_timing_checks(inject):
     assert c["post_validation"]["result"] == "ok", c["post_validation"]
     assert c["post_validation"]["transport"] == c["transport"]
     fp = c["fused_post_check"]
-    assert fp is not None and fp["steps"] >= 200
+    assert fp is not None and fp["steps"] >= 200, (c.get("fused_ab_ms"), r.stderr[-3000:])
     if inject:
         assert fp["result"] == "mismatch" and "fallback" in fp
         assert c["fused_halo"] is False

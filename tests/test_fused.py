@@ -248,3 +248,31 @@ def test_fused_default_graph_steps(gpu):
     torch.cuda.synchronize()
     assert torch.equal(a.T, b.T) and torch.equal(a.T, c.T)
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_graph_after_odd_step_counts(gpu):
+    """run() after odd step counts (the graph reads the capture's T first),
+    plain and fused, and after a restore-like write with mark_modified."""
+    a, b = _pair((24, 22, 64), (1, 1, 1), torch.float64, 0)
+    c = Diffusion3D(dtype=torch.float64, variant=0)
+    b.capture(steps=4)  # one priming step each
+    c.capture(steps=4)
+    a.run(1)
+    for k in (5, 3, 8, 7):
+        for m in (a, b, c):
+            m.run(k)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    assert torch.equal(a.T, b.T) and torch.equal(a.T, c.T)
+    for m in (b, c):
+        m.T.copy_(a.T)
+        m.T2.copy_(a.T2)
+        m.mark_modified()
+    for m in (a, b, c):
+        m.run(9)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T) and torch.equal(a.T, c.T)
+    igg.finalize_global_grid(finalize_MPI=False)
