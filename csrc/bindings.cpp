@@ -564,6 +564,11 @@ PYBIND11_MODULE(_igg_native, m) {
            py::arg("ny"), py::arg("dtk"), py::arg("dt_rho"), py::arg("rdx"), py::arg("rdy"), py::arg("elem_bytes"),
            py::arg("stream"), py::arg("entry") = false)
       .def("check_error", &FusedAcoustic::check_error)
+      .def("set_step_sync", &FusedAcoustic::set_step_sync, py::arg("mode"),
+           "Step synchronisation: -1 default, 0 inside the fused kernel, 1 sync kernel (same on every rank).")
+      .def_property_readonly("in_kernel_sync", &FusedAcoustic::in_kernel_sync)
+      .def("flag", [](FusedAcoustic& f, int i) { return f.flag(i); }, py::arg("index"),
+           "Word `index` of this rank's flag block (PutFlags: 0 EPOCH = completed steps, 2 COUNT).")
       .def("close", &FusedAcoustic::close);
   m.def("acoustic2d_set_variant", &acoustic2d_set_variant);
   m.def("acoustic2d_set_chunk", &acoustic2d_set_chunk);
@@ -645,6 +650,11 @@ PYBIND11_MODULE(_igg_native, m) {
       .def_property_readonly("zpitch", &FusedHalo::zpitch)
       .def_property_readonly("n_peers", &FusedHalo::n_peers)
       .def("check_error", [](FusedHalo& f) { f.mesh().check_error(); })
+      .def("set_step_sync", &FusedHalo::set_step_sync, py::arg("mode"),
+           "Step synchronisation: -1 default, 0 inside the fused kernel, 1 sync kernel (same on every rank).")
+      .def_property_readonly("in_kernel_sync", &FusedHalo::in_kernel_sync)
+      .def("flag", [](FusedHalo& f, int i) { return f.mesh().read_flag(i); }, py::arg("index"),
+           "Word `index` of this rank's flag block (PutFlags: 0 EPOCH = completed steps, 2 COUNT).")
       .def("close", [](FusedHalo& f) { f.close(); });
   m.def("split_boundary", [](const Int3& n, const std::array<std::array<bool, 2>, 3>& active,
                              const Int3& w) {

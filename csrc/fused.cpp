@@ -102,10 +102,23 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
     if (a.n[d] != n_[d]) fail("FusedHalo.step: field shape does not match the fused halo's local grid");
   if (a.elem_bytes != elem_) fail("FusedHalo.step: field dtype does not match the fused halo");
   if (entry) sync(stream);  // entry barrier (fused.hpp)
-  launch_diffusion3d_fused(a, io(step, primed, a.t2, (mode & 4) != 0), variant, mode, stream);
-  sync(stream);
+  HaloIOArgs x = io(step, primed, a.t2, (mode & 4) != 0);
+  // Step synchronisation inside the kernel (put.hpp StepSync), else the sync
+  // kernel after it (IGG_FUSED_SYNC_KERNEL=1, or a launch that cannot count
+  // its exchanging waves).
+  bool used = false;
+  if (in_kernel_sync()) {
+    x.sync = step_sync_from(sync_);
+    x.sync_used = &used;
+  }
+  launch_diffusion3d_fused(a, x, variant, mode, stream);
+  if (!used) sync(stream);
 }
 
 void FusedHalo::sync(hipStream_t stream) const { launch_put_sync(sync_, stream); }
+
+bool FusedHalo::in_kernel_sync() const {
+  return sync_mode_ < 0 ? step_sync_in_kernel(mesh_->shares_device()) : sync_mode_ == 0;
+}
 
 }  // namespace igg

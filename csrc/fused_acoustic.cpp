@@ -75,12 +75,22 @@ void FusedAcoustic::step(const AcousticArgs& a, hipStream_t stream, bool entry) 
       h.send_y[s] = reinterpret_cast<uintptr_t>(fields_.at(r)[2 + k] + (s == 0 ? ny_ : 0) * eb);
     }
   }
+  // Step synchronisation inside the kernel (put.hpp StepSync: no sync kernel
+  // on the stream), or the 1-wave sync kernel after it (IGG_FUSED_SYNC_KERNEL=1).
+  const bool sync_kernel = !in_kernel_sync();
+  if (!sync_kernel) h.sync = step_sync_from(sync_);
   if (entry) launch_put_sync(sync_, stream);  // entry barrier
   launch_acoustic2d_fused(a, h, stream);
-  launch_put_sync(sync_, stream);
+  if (sync_kernel) launch_put_sync(sync_, stream);
 }
 
 void FusedAcoustic::check_error() const { mesh_->check_error(); }
+
+uint64_t FusedAcoustic::flag(int index) const { return mesh_->read_flag(index); }
+
+bool FusedAcoustic::in_kernel_sync() const {
+  return sync_mode_ < 0 ? step_sync_in_kernel(mesh_->shares_device()) : sync_mode_ == 0;
+}
 
 void FusedAcoustic::close() {
   fields_.clear();

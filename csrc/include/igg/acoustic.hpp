@@ -48,6 +48,7 @@ struct AcousticHalo {
   uintptr_t send_y[2] = {0, 0};  // Vy2 columns (one element per row, pitch ny+1)
   bool nb_x[2] = {false, false}, nb_y[2] = {false, false};
   int plain_stores = 0;  // debug (IGG_FUSED_PLAIN_STORES=1): plain instead of system-scope remote stores
+  StepSync sync;  // in-kernel step synchronisation (put.hpp); set by FusedAcoustic
 };
 
 void launch_acoustic2d(const AcousticArgs& a, hipStream_t stream);
@@ -86,6 +87,10 @@ class FusedAcoustic {
   // overtake this rank's own earlier writes to the fields: FusedHalo::step).
   void step(const AcousticArgs& a, hipStream_t stream, bool entry = false);
   void check_error() const;
+  uint64_t flag(int index) const;  // own flag word (PutFlags), host read
+  // Step synchronisation form (FusedHalo::set_step_sync).
+  void set_step_sync(int mode) { sync_mode_ = mode; }
+  bool in_kernel_sync() const;
   void close();
 
  private:
@@ -94,6 +99,7 @@ class FusedAcoustic {
   int elem_;
   std::array<std::array<int, 2>, 2> nb_;
   PutSync sync_{};
+  int sync_mode_ = -1;
   std::vector<std::vector<char*>> fields_;  // [rank][vx_a, vx_b, vy_a, vy_b]
 };
 

@@ -1,0 +1,80 @@
+#pragma once
+// Device-side flag primitives of the one-sided exchanges (device code): the
+// flag words live in uncached memory (PutFlags, put.hpp), so relaxed
+// system-scope accesses reach memory on every poll. Shared by the put sync
+// kernels (put_kernels.hip) and the in-kernel step synchronisation of the
+// fused acoustic exchange (acoustic_kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "igg/put.hpp"
+
+namespace igg {
+
+// Relaxed system-scope store: flag stores follow one explicit system-scope
+// release fence where one is needed (a release store per flag would emit its
+// own L2 write-back, ~1.7 us each on gfx950).
+__device__ __forceinline__ void store_sys_relaxed(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ uint64_t load_sys_relaxed(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Spin until *p >= v; false (and `code` recorded in the sticky ERROR word of
+// `my_flags`) on timeout. The poll is relaxed (system scope: it bypasses the
+// caches and sees the peer's store); the caller issues the acquire fence it
+// needs after the spin (an acquire load per poll would invalidate the caches
+// on every iteration). Once an exchange has timed out (ERROR set), later waits
+// give up at once: a dead or diverged peer costs ONE timeout, not one per step
+// (the host reports the error at its next check and the data is invalid
+// anyway).
+__device__ inline bool spin_geq(const uint64_t* p, uint64_t v, uint64_t* my_flags, int64_t timeout_ticks,
+                                uint64_t code) {
+  const long long t0 = wall_clock64();
+  while (load_sys_relaxed(p) < v) {
+    __builtin_amdgcn_s_sleep(2);
+    if (load_sys_relaxed(my_flags + PutFlags::ERROR) != 0) return false;
+    if (wall_clock64() - t0 > timeout_ticks) {
+      uint64_t expected = 0;
+      __hip_atomic_compare_exchange_strong(my_flags + PutFlags::ERROR, &expected, code, __ATOMIC_RELAXED,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+  }
+  return true;
+}
+
+// StepSync (put.hpp), at the start of an exchanging wave: returns c, the
+// number of completed steps (this is step c + 1), after every neighbour has
+// completed step c. EPOCH is advanced only by the last exchanging wave of this
+// kernel, after every exchanging wave read it. The system acquire drops any
+// stale copy of a received halo from this CU's L1 before the sweep loads it
+// (the L2 copies were invalidated by the writers' coherent stores).
+__device__ inline uint64_t step_sync_enter(const StepSync& s, int lane) {
+  const uint64_t c = load_sys_relaxed(s.my_flags + PutFlags::EPOCH);
+  if (lane < s.n_peers)
+    spin_geq(s.my_flags + PutFlags::ARRIVED + s.peer_rank[lane], c, s.my_flags, s.timeout_ticks, 0x300 + lane);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return c;
+}
+
+// At the end of an exchanging wave: its system-scope sends acknowledged and
+// every load returned (s_waitcnt 0), it counts itself; the last one publishes
+// step c + 1 (ARRIVED at every neighbour, then own EPOCH).
+__device__ inline void step_sync_exit(const StepSync& s, int lane, uint64_t c) {
+  __builtin_amdgcn_s_waitcnt(0);
+  uint64_t old = 0;
+  if (lane == 0)
+    old = __hip_atomic_fetch_add(s.my_flags + PutFlags::COUNT, uint64_t{1}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0);
+  if (old + 1 == static_cast<uint64_t>(s.feat_waves)) {
+    if (lane == 0) __hip_atomic_store(s.my_flags + PutFlags::COUNT, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < s.n_peers) store_sys_relaxed(s.peer_flags[lane] + PutFlags::ARRIVED + s.my_rank, c + 1);
+    if (lane == 0) store_sys_relaxed(s.my_flags + PutFlags::EPOCH, c + 1);
+  }
+}
+
+}  // namespace igg

@@ -4,18 +4,19 @@
 // The reference exchanges halos after the compute (update_halo!, pack ->
 // Isend/Irecv -> unpack per dimension, src/update_halo.jl:32-78); on one node
 // of MI355X every GPU can store straight into a neighbour's HBM over xGMI. So
-// a fused step is two launches on one stream:
-//   1. the stencil (launch_diffusion3d_fused): while sweeping the interior it
-//      stores the planes each neighbour needs (x=1/n0-2, y=1/n1-2, z=1/n2-2)
-//      into that neighbour's IPC-mapped, fine-grained arena, and reads its
-//      own face halos from its arena instead of from the field; every wave
-//      that stored to a peer ends with a system-scope release (wave_release
-//      in fused_impl.hpp);
-//   2. the put-transport sync kernel (1 wave): publish "my step arrived" at
-//      every neighbour, wait for theirs (bounded spins, error flag on timeout).
+// a fused step is ONE launch on the caller's stream: the stencil
+// (launch_diffusion3d_fused) stores, while sweeping the interior, the planes
+// each neighbour needs (x=1/n0-2, y=1/n1-2, z=1/n2-2) into that neighbour's
+// IPC-mapped, fine-grained arena with system-scope stores (st_sys), and reads
+// its own face halos from its arena instead of from the field. Its exchanging
+// waves also synchronise the step with the neighbours (put.hpp StepSync: wait
+// for the neighbours' previous step, the last one publishes this step; bounded
+// spins, error flag on timeout). Where another rank shares the GPU, or with
+// IGG_FUSED_SYNC_KERNEL=1, a 1-wave sync kernel after the stencil does that
+// instead (waiting waves could hold the compute units the other rank needs).
 // The arena has two halves: step i writes half i&1 and reads half (i-1)&1, so
 // a neighbour may run one step ahead without overwriting data still in use;
-// the per-step neighbour barrier of the sync kernel bounds the skew to one.
+// the per-step neighbour synchronisation bounds the skew to one.
 // The fields' own halo planes are not touched; sync_halo (update_halo_ of T)
 // materialises them when a caller needs them (gather, output, mode switch).
 // Direct z (mode bit 4, set_fields): the z faces skip the arena and land in
@@ -23,7 +24,7 @@
 // step reads like any other element. Ordering: a neighbour writes my buffer k
 // (halo elements only) during the step in which my stencil writes buffer k's
 // interior and reads buffer 1-k; my previous step (which read buffer k)
-// finished before that neighbour's sync kernel let it start this step.
+// finished before that neighbour's step synchronisation let it start this step.
 // Coherence: the halo element shares a cache line with interior elements my
 // own kernel is writing at the same time, from another device. HIP defines
 // that for fine-grained memory only, so across devices the fields must be
@@ -65,8 +66,8 @@ class FusedHalo {
   // neighbour's t2 is its buffer k".
   void set_fields(uintptr_t a, uintptr_t b);
   bool has_fields() const { return !fields_.empty(); }
-  // Stencil with fused send/receive + sync kernel, on `stream`. `entry`: a
-  // sync kernel first - the neighbours' remote stores of this step must not
+  // Stencil with fused send/receive and step synchronisation, on `stream`.
+  // `entry`: a sync kernel first - the neighbours' remote stores of this step must not
   // overtake this rank's own earlier writes to the fields or the arena (a
   // restore, a switch into fused mode); every rank passes the same flag.
   void step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed, hipStream_t stream,
@@ -78,6 +79,11 @@ class FusedHalo {
   }
   // Only the sync kernel (e.g. to rehearse the barrier cost).
   void sync(hipStream_t stream) const;
+  // Step synchronisation inside the fused kernel (put.hpp StepSync) or by the
+  // sync kernel after it: -1 the default (step_sync_in_kernel), 0 in the
+  // kernel, 1 sync kernel. Every rank must use the same form.
+  void set_step_sync(int mode) { sync_mode_ = mode; }
+  bool in_kernel_sync() const;
 
   int64_t region_offset(int d, int s) const { return off_[d][s]; }  // elements within a half
   int64_t half_elems() const { return half_; }
@@ -97,6 +103,7 @@ class FusedHalo {
   int64_t off_[3][2];
   int64_t half_ = 0, zp_ = 0;
   PutSync sync_{};
+  int sync_mode_ = -1;
   std::vector<std::vector<char*>> fields_;  // [rank][k]: ping-pong buffer k (set_fields)
 };
 

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "igg/devsync.hpp"
 #include "igg/stencil.hpp"
 #include "igg/sysstore.hpp"
 
@@ -85,6 +86,7 @@ struct HxScal {
   int64_t* stamps;
   int force_sel;
   int peel;  // send mode bit 8: sweep the exchanged x planes of a chunk separately (kernel below)
+  StepSync sync;  // in-kernel step synchronisation (put.hpp; my_flags null: a sync kernel follows)
 };
 
 // Writer side of the cross-device hand-off: every store into peer memory
@@ -533,6 +535,11 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     int sel = __builtin_amdgcn_readfirstlane((wx ? 1 : 0) | (wyy ? 2 : 0) | (wzz ? 4 : 0));
     if (a.force_sel >= 0) sel = a.force_sel;
     const int64_t t_start = a.stamps ? wall_clock64() : 0;
+    // The exchanging waves (sel != 0) synchronise the step with the
+    // neighbours (StepSync, put.hpp); the others never touch memory a
+    // neighbour reads or writes. (Counted on the host by hx_feature_waves.)
+    const bool ks = a.sync.my_flags != nullptr && sel != 0;
+    const uint64_t kc = ks ? step_sync_enter(a.sync, threadIdx.x & 63) : 0;
     // Peel (a.peel): an x-chunk wave needs the x exchange only at x = 1 (reads
     // plane 0 from the arena, sends plane 1) and x = n0-2 (sends it, reads
     // plane n0-1); the planes in between are swept with the x features
@@ -564,6 +571,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
         default: IGG_HX_SWEEP_R(FEAT); break;
       }
     }
+    if (ks) step_sync_exit(a.sync, threadIdx.x & 63, kc);
     if (a.stamps) {
       // one vector store per wave (lane 0; lane-dependent address -> VGPR store)
       const int lane = threadIdx.x & 63;
@@ -591,6 +599,35 @@ int resident(const void* kernel, int block, size_t lds = 0) {
   const int r = std::max(1, occ) * std::max(1, cus);
   cache.emplace_back(kernel, r);
   return r;
+}
+
+// The number of waves of a launch that run an exchange form (sel != 0 in
+// diffusion3d_hx_kernel): the same per-wave rule on the host. The rule is
+// separable - the x part depends on the chunk, the y part on the wave's rows,
+// the z part on its z tile - so the waves with no feature are a product.
+template <int BY, int RY, int VZ, int BZ, int FEAT>
+int64_t hx_feature_waves(int64_t n0, int64_t n1, int64_t n2, int64_t ch, int64_t nty, int64_t ntz,
+                         const HaloIOArgs& io) {
+  constexpr int FX = FEAT & (1 | 64), FY = FEAT & (2 | 128), FZ = FEAT & (4 | 8);
+  constexpr int W = 64 * VZ * BZ;
+  auto on = [&](int d, int s) { return io.in[d][s] != 0 || io.out[d][s] != 0; };
+  const int64_t nch = (n0 - 2 + ch - 1) / ch;
+  int64_t qx = 0, qy = 0, qz = 0;  // counts WITHOUT the feature
+  for (int64_t cx = 0; cx < nch; ++cx) {
+    const int64_t xs = 1 + cx * ch, xe = std::min(xs + ch, n0 - 1);
+    qx += !(FX != 0 && ((xs <= 1 && on(0, 0)) || (xe >= n0 - 2 && on(0, 1))));
+  }
+  for (int64_t ty = 0; ty < nty; ++ty)
+    for (int wy = 0; wy < BY; ++wy) {
+      const int64_t y0 = 1 + ty * (BY * RY) + wy * RY, nv = std::min<int64_t>(RY, n1 - 1 - y0);
+      qy += !(FY != 0 && ((y0 <= 1 && on(1, 0)) || (y0 + nv >= n1 - 1 && on(1, 1))));
+    }
+  for (int64_t tz = 0; tz < ntz; ++tz)
+    for (int wz = 0; wz < BZ; ++wz) {
+      const int64_t zt = tz * W + wz * (64 * VZ);
+      qz += !(FZ != 0 && ((zt == 0 && on(2, 0)) || (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ && on(2, 1))));
+    }
+  return nch * nty * BY * ntz * BZ - qx * qy * qz;
 }
 
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
@@ -623,6 +660,16 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   a.stamps = g_hx_stamps;
   a.force_sel = g_hx_force_sel;
   a.peel = peel ? 1 : 0;
+  a.sync = StepSync{};
+  // In-kernel step sync: the specialised kernel only (per-wave feature
+  // classes), and not under the diagnostics that override the classes.
+  constexpr int FXYZ = FEAT & (1 | 2 | 4 | 8 | 64 | 128);
+  if (io.sync.my_flags && FXYZ != 0 && (FEAT & 2048) == 0 && !a.stamps && a.force_sel < 0) {
+    a.sync = io.sync;
+    a.sync.feat_waves = hx_feature_waves<BY, RY, VZ, BZ, FEAT>(n0, n1, n2, a.ch, a.nty, a.ntz, io);
+    if (a.sync.feat_waves < 1) a.sync.my_flags = nullptr;
+  }
+  if (io.sync_used) *io.sync_used = a.sync.my_flags != nullptr;
   auto in = [&](int k, int s) { return reinterpret_cast<const T*>(io.in[k][s]); };
   auto out = [&](int k, int s) { return reinterpret_cast<T*>(io.out[k][s]); };
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(block), lds, stream,

@@ -65,10 +65,16 @@ class PeerMesh {
   std::vector<std::vector<char*>> map_buffers(const std::vector<uintptr_t>& mine);
   // Collective teardown (also run by the destructor without the collectives).
   void close();
+  // Some other rank of the mesh runs on this rank's GPU (same host and PCI
+  // bus id; determined collectively at construction). In-kernel waits for a
+  // neighbour are then unsafe: the waiting kernel can hold the compute units
+  // the neighbour's kernel needs (put.hpp StepSync).
+  bool shares_device() const { return shares_device_; }
 
  private:
   void exchange_handles(bool flags_too);
   int rank_, nranks_;
+  bool shares_device_ = false;
   AllGather allgather_;
   uint64_t* flags_ = nullptr;
   char* arena_ = nullptr;

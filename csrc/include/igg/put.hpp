@@ -32,6 +32,7 @@ constexpr int PUT_MAX_PEERS = 27;
 struct PutFlags {
   static constexpr int EPOCH = 0;     // completed exchanges (the running one is EPOCH + 1)
   static constexpr int ERROR = 1;     // 0 ok, else 1 + code of the first timeout
+  static constexpr int COUNT = 2;     // exchanging waves retired in the running step (in-kernel step sync)
   static constexpr int ARRIVED = 8;   // [ARRIVED + r]: last epoch rank r's data arrived
   __host__ __device__ static inline int freed(int nranks) { return ARRIVED + nranks; }  // [freed + r]
   __host__ __device__ static inline int words(int nranks) { return ARRIVED + 2 * nranks; }
@@ -47,6 +48,35 @@ struct PutSync {
   int my_rank, nranks;
   int64_t timeout_ticks;                  // wall_clock64 ticks
 };
+
+// In-kernel step synchronisation of the fused exchanges (FusedHalo,
+// FusedAcoustic), replacing the sync kernel after every step: only the
+// exchanging waves of the step kernel take part (those whose tile reads a
+// received halo or stores a sent one; every other wave touches no memory a
+// neighbour reads or writes). Each of them first waits until every neighbour
+// has completed the previous step (ARRIVED[nb] >= own EPOCH: its sends of the
+// halos the wave reads have arrived, and its reads of the memory the wave
+// overwrites in it are done), and the last one of them to retire (the COUNT
+// word reaches `feat_waves`) publishes ARRIVED = EPOCH + 1 at the neighbours
+// and advances EPOCH. docs/COHERENCE.md has the ordering argument.
+// my_flags == nullptr: not used (a sync kernel follows the step kernel).
+constexpr int STEP_SYNC_MAX_PEERS = 6;  // face neighbours of a 3-D rank
+struct StepSync {
+  uint64_t* my_flags = nullptr;
+  uint64_t* peer_flags[STEP_SYNC_MAX_PEERS] = {};
+  int peer_rank[STEP_SYNC_MAX_PEERS] = {};
+  int n_peers = 0, my_rank = 0;
+  int64_t timeout_ticks = 0;
+  int64_t feat_waves = 0;  // exchanging waves of the launch (set by the launcher)
+};
+// The StepSync of a face-neighbour PutSync (every peer both sends and receives).
+StepSync step_sync_from(const PutSync& s);
+// Whether a fused exchange synchronises its steps inside the step kernel.
+// IGG_FUSED_SYNC_KERNEL unset: yes unless another rank of the mesh shares
+// this rank's GPU (its waiting waves could starve that rank's kernel); "1":
+// never (the sync kernel after every step); "0": always (tests whose kernels
+// cannot fill the GPU).
+bool step_sync_in_kernel(bool shares_device);
 
 void launch_put_begin(const PutSync& s, hipStream_t stream);
 void launch_put_sync(const PutSync& s, hipStream_t stream);

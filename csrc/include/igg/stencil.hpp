@@ -16,6 +16,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "igg/common.hpp"
+#include "igg/put.hpp"
 
 namespace igg {
 
@@ -63,6 +64,11 @@ struct HaloIOArgs {
   uintptr_t out[3][2];
   int64_t zpitch;
   int64_t zrow;
+  // In-kernel step synchronisation (put.hpp StepSync; FusedHalo): the launch
+  // takes it when it can count its exchanging waves and then sets *sync_used
+  // (otherwise the caller follows the kernel with the sync kernel).
+  StepSync sync;
+  bool* sync_used = nullptr;
 };
 bool diffusion3d_fused_variant_ok(int v);
 // Diagnostics of the fused kernel: per-wave {feature class, start, end, hw id}

@@ -9,44 +9,44 @@
 // every storing wave with s_waitcnt vmcnt(0) before the flag that publishes
 // the data is set (next kernel on the stream).
 //
-// HIP has no builtin for these cache-policy bits on a flat/global store, so
-// the stores are inline asm, which the compiler's hazard recognizer does not
-// see: a store of more than 64 bits reads its data VGPRs after issue, and a
-// VALU write to those VGPRs right behind it (the "VMEM store data" hazard)
-// would change the bytes in flight - observed on MI355X as the fourth dword of
-// dwordx4 stores carrying the NEXT value (tools/acoustic_fused_debug.py,
-// profiles/r3_acoustic/). The s_nop after every dwordx4 store covers the
-// required wait states. No memory clobber: the destinations never alias
-// anything the kernel reads (restrict arguments), so the compiler may keep
-// scheduling loads across them; as untracked vector-memory operations they
-// only make its vmcnt waits more conservative (in-order vmcnt on gfx9).
+// The stores are relaxed system-scope atomic stores of 1, 2, 4 or 8 bytes (a
+// wider value is split), which the compiler emits as `global_store_{byte,
+// short,dword,dwordx2} ... sc0 sc1` and schedules like any other memory instruction. (Rounds 2-3 used
+// inline-asm `global_store_dwordx4 ... sc0 sc1` for 16-B vectors: the
+// compiler's hazard recognizer does not see inside inline asm, and with the
+// fused kernels at the 256-VGPR limit (spilling to AGPRs) a wrong interior
+// value appeared in one fused form after an unrelated code change,
+// deterministic per binary; profiles/r3_sysstore/.)
 #include <hip/hip_runtime.h>
+
+#include <cstdint>
 
 namespace igg {
 
 template <typename V>
 __device__ __forceinline__ void st_sys(V* p, const V& v) {
-  static_assert(sizeof(V) == 1 || sizeof(V) == 2 || sizeof(V) == 4 || sizeof(V) == 8 || sizeof(V) == 16 ||
-                    sizeof(V) == 32,
-                "st_sys: 1, 2, 4, 8, 16 or 32 bytes");
-  using U4 = unsigned __attribute__((ext_vector_type(4)));
-  if constexpr (sizeof(V) == 32) {
-    struct P2 { U4 lo, hi; };
-    const P2 h = __builtin_bit_cast(P2, v);
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 4" ::"v"(p), "v"(h.lo));
-    asm volatile("global_store_dwordx4 %0, %1, off offset:16 sc0 sc1\n\ts_nop 4" ::"v"(p), "v"(h.hi));
-  } else if constexpr (sizeof(V) == 16) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 4" ::"v"(p), "v"(__builtin_bit_cast(U4, v)));
-  } else if constexpr (sizeof(V) == 8) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(__builtin_bit_cast(unsigned long long, v)));
-  } else if constexpr (sizeof(V) == 4) {
-    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(__builtin_bit_cast(unsigned, v)));
+  static_assert(sizeof(V) == 1 || sizeof(V) == 2 || (sizeof(V) % 4 == 0 && sizeof(V) <= 32),
+                "st_sys: 1, 2 or 4..32 bytes (a multiple of 4)");
+  if constexpr (sizeof(V) == 1) {
+    __hip_atomic_store(reinterpret_cast<uint8_t*>(p), __builtin_bit_cast(uint8_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   } else if constexpr (sizeof(V) == 2) {
-    asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p),
-                 "v"(static_cast<unsigned>(__builtin_bit_cast(unsigned short, v))));
+    __hip_atomic_store(reinterpret_cast<uint16_t*>(p), __builtin_bit_cast(uint16_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  } else if constexpr (sizeof(V) % 8 == 0) {
+    struct W { uint64_t w[sizeof(V) / 8]; };
+    const W x = __builtin_bit_cast(W, v);
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+#pragma unroll
+    for (int i = 0; i < static_cast<int>(sizeof(V) / 8); ++i)
+      __hip_atomic_store(q + i, x.w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
-    asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p),
-                 "v"(static_cast<unsigned>(__builtin_bit_cast(unsigned char, v))));
+    struct W { uint32_t w[sizeof(V) / 4]; };
+    const W x = __builtin_bit_cast(W, v);
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+#pragma unroll
+    for (int i = 0; i < static_cast<int>(sizeof(V) / 4); ++i)
+      __hip_atomic_store(q + i, x.w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

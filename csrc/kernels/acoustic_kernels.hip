@@ -8,9 +8,12 @@
 // loaded by the adjacent lane or wave, so they come from L1/L2, not HBM.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "igg/acoustic.hpp"
 #include "igg/common.hpp"
 #include "igg/copy.hpp"
+#include "igg/devsync.hpp"
 #include "igg/sysstore.hpp"
 
 namespace igg {
@@ -164,9 +167,12 @@ __device__ __forceinline__ void st_remote(T* p, const T& v, int plain) {
   else st_sys(p, v);
 }
 
-template <typename T, int VJ, bool FUSED>
-__global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticArgs a, int64_t ch,
-                                                                     AcousticHalo h) {
+// The rows [i0, i1) of one wave's segment. FEAT: the exchange features of the
+// fused step (sends, faces left to the neighbours) are compiled in; a wave runs
+// that form only if its tile touches them (acoustic2d_vmarch_kernel).
+template <typename T, int VJ, bool FEAT>
+__device__ __forceinline__ void vmarch_rows(const AcousticArgs& a, const AcousticHalo& h, int64_t seg,
+                                            int64_t i0, int64_t i1) {
   // No FMA contraction: every value is rounded per operation, so a point gets
   // bitwise the same result wherever it is computed - in the march loop or in
   // a chunk's first-row recomputation of P2(i-1), on this rank or on the
@@ -178,13 +184,7 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
   typedef T VU __attribute__((ext_vector_type(VJ), aligned(sizeof(T))));
   constexpr int64_t OWNV = 62 * VJ;
   const int lane = threadIdx.x & 63;
-  const int64_t wave = static_cast<int64_t>(blockIdx.x) * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nx = a.nx, ny = a.ny, sy = ny + 1;
-  const int64_t nseg = (ny + 1 + OWNV - 1) / OWNV;
-  const int64_t seg = wave % nseg, chunk = wave / nseg;
-  const int64_t i0 = chunk * ch;
-  if (i0 > nx) return;  // wave-uniform
-  const int64_t i1 = min(i0 + ch, nx + 1);
   const int64_t j0 = seg * OWNV + static_cast<int64_t>(lane - 1) * VJ;  // first column of this lane
   const bool own = lane >= 1 && lane <= 62 && j0 <= ny;
   const bool cells = j0 + VJ <= ny && j0 >= 0;   // VJ cell / x-face columns
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
 #pragma unroll
           for (int e = 0; e < VJ; ++e) vxo[e] = (i >= 1) ? vx_i[e] - dt_rho * (pc[e] - p2_prev[e]) * rdx : vx_i[e];
           __builtin_nontemporal_store(pc, reinterpret_cast<V*>(p2 + i * ny + j0));
-          if constexpr (FUSED) {
+          if constexpr (FEAT) {
             // face 0 of a side with a neighbour: the neighbour stores it
             if (!(i == 0 && h.nb_x[0])) __builtin_nontemporal_store(vxo, reinterpret_cast<V*>(vx2 + i * ny + j0));
             if (i == 2 && h.send_x[0]) st_remote(reinterpret_cast<V*>(h.send_x[0]) + j0 / VJ, vxo, h.plain_stores);
@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
             *reinterpret_cast<VU*>(vy2 + i * sy + j0) = vyo;
           }
         } else if (last) {
-          if (!FUSED || !h.nb_y[1]) vy2[i * sy + ny] = vy_h[0];
+          if (!FEAT || !h.nb_y[1]) vy2[i * sy + ny] = vy_h[0];
         }
       }
       vx_i = vx_n;
@@ -282,12 +282,56 @@ __global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticA
       vx_n = vx_n1;
       pp = pp1;
     } else if (own && cells) {  // i == nx: the last x-faces are boundary faces
-      if (!FUSED || !h.nb_x[1]) *reinterpret_cast<V*>(vx2 + i * ny + j0) = vx_i;
+      if (!FEAT || !h.nb_x[1]) *reinterpret_cast<V*>(vx2 + i * ny + j0) = vx_i;
     }
   }
-  // System-scope remote stores acknowledged before the wave retires (the sync
-  // kernel that publishes the arrival flags runs next on this stream).
-  if constexpr (FUSED) __builtin_amdgcn_s_waitcnt(0);
+}
+
+// Does the wave of segment `seg` / rows [i0, i1) run the exchange form? Rows
+// 0..2 and nx-2..nx (x faces and sends), segment 0 (columns 0..2) and the
+// segments holding columns ny-2..ny (they may straddle the last two). Host
+// and device use the same rule (the in-kernel step sync counts these waves).
+__host__ __device__ inline bool vmarch_feature_rows(int64_t i0, int64_t i1, int64_t nx) {
+  return i0 <= 2 || i1 > nx - 2;
+}
+__host__ __device__ inline bool vmarch_feature_seg(int64_t seg, int64_t ny, int64_t ownv) {
+  return seg == 0 || seg >= (ny - 2) / ownv;
+}
+__host__ __device__ inline bool vmarch_feature(int64_t seg, int64_t i0, int64_t i1, int64_t nx, int64_t ny,
+                                               int64_t ownv) {
+  return vmarch_feature_seg(seg, ny, ownv) || vmarch_feature_rows(i0, i1, nx);
+}
+
+template <typename T, int VJ, bool FUSED>
+__global__ void __launch_bounds__(64 * WAVES) acoustic2d_vmarch_kernel(AcousticArgs a, int64_t ch,
+                                                                     AcousticHalo h) {
+  constexpr int64_t OWNV = 62 * VJ;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nx = a.nx, ny = a.ny;
+  const int64_t nseg = (ny + 1 + OWNV - 1) / OWNV;
+  const int64_t seg = wave % nseg, chunk = wave / nseg;
+  const int64_t i0 = chunk * ch;
+  if (i0 > nx) return;  // wave-uniform
+  const int64_t i1 = min(i0 + ch, nx + 1);
+  if constexpr (FUSED) {
+    // Only the tiles at the exchanged faces carry the exchange code; the
+    // others run the plain sweep (wave-uniform branch). Exchange code merely
+    // present in the hot loop costs every wave (the diffusion kernel's
+    // measurement: profiles/r2_fused_spec/).
+    if (vmarch_feature(seg, i0, i1, nx, ny, OWNV)) {
+      const int lane = threadIdx.x & 63;
+      const uint64_t c = h.sync.my_flags ? step_sync_enter(h.sync, lane) : 0;
+      vmarch_rows<T, VJ, true>(a, h, seg, i0, i1);
+      // System-scope remote stores acknowledged (they reached the owner's
+      // memory) before the wave retires: the sync kernel that publishes the
+      // arrival flags runs next on this stream, or the last exchanging wave
+      // publishes them (step_sync_exit).
+      if (h.sync.my_flags) step_sync_exit(h.sync, lane, c);
+      else __builtin_amdgcn_s_waitcnt(0);
+      return;
+    }
+  }
+  vmarch_rows<T, VJ, false>(a, h, seg, i0, i1);
 }
 
 template <typename T>
@@ -372,13 +416,24 @@ void launch_acoustic2d_fused(const AcousticArgs& a, const AcousticHalo& h, hipSt
   const int vj = a.elem_bytes == 4 ? 4 : 2;
   if (a.ny % vj != 0 || a.ny < 2 * vj || a.nx < 5 || a.ny < 5)
     fail("acoustic2d (fused halo): needs ny % ", vj, " == 0 and nx, ny >= 5");
+  if (h.sync.my_flags && (h.sync.n_peers < 1 || h.sync.n_peers > 4))
+    fail("acoustic2d (fused halo): in-kernel sync needs 1..4 peers (got ", h.sync.n_peers, ")");
   const int64_t ch = g_march_ch > 0 ? g_march_ch : VMARCH_CH;
-  const int64_t nseg = (a.ny + 1 + 62 * vj - 1) / (62 * vj), nch = (a.nx + 1 + ch - 1) / ch;
+  const int64_t ownv = 62 * vj;
+  const int64_t nseg = (a.ny + 1 + ownv - 1) / ownv, nch = (a.nx + 1 + ch - 1) / ch;
+  // exchanging waves (the in-kernel step sync waits for this many to count)
+  int64_t fseg = 0, feat = 0;
+  for (int64_t sg = 0; sg < nseg; ++sg) fseg += vmarch_feature_seg(sg, a.ny, ownv) ? 1 : 0;
+  for (int64_t c = 0; c < nch; ++c)
+    feat += vmarch_feature_rows(c * ch, std::min(c * ch + ch, a.nx + 1), a.nx) ? nseg : fseg;
+  AcousticHalo hh = h;
+  hh.sync.feat_waves = feat;
+  if (feat < 1) hh.sync.my_flags = nullptr;  // unreachable (rows 0..2 always exchange); keep the sync kernel form
   const dim3 grid(static_cast<unsigned>((nseg * nch + WAVES - 1) / WAVES));
   if (a.elem_bytes == 8)
-    hipLaunchKernelGGL((acoustic2d_vmarch_kernel<double, 2, true>), grid, dim3(64 * WAVES), 0, stream, a, ch, h);
+    hipLaunchKernelGGL((acoustic2d_vmarch_kernel<double, 2, true>), grid, dim3(64 * WAVES), 0, stream, a, ch, hh);
   else
-    hipLaunchKernelGGL((acoustic2d_vmarch_kernel<float, 4, true>), grid, dim3(64 * WAVES), 0, stream, a, ch, h);
+    hipLaunchKernelGGL((acoustic2d_vmarch_kernel<float, 4, true>), grid, dim3(64 * WAVES), 0, stream, a, ch, hh);
   IGG_HIP_CHECK(hipGetLastError());
 }
 

@@ -1,43 +1,19 @@
 // Put-transport synchronisation kernels (one workgroup of one wave each).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "igg/common.hpp"
+#include "igg/devsync.hpp"
 #include "igg/put.hpp"
 
 namespace igg {
 namespace {
 
-// Relaxed system-scope store: flag stores follow one explicit system-scope
-// release fence (a release store per flag would emit its own L2 write-back,
-// ~1.7 us each on gfx950).
-__device__ __forceinline__ void store_sys_relaxed(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ uint64_t load_sys_relaxed(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Spin until *p >= v; false (and an error code recorded) on timeout. The poll
-// is relaxed (system scope: it bypasses the caches and sees the peer's store);
-// one acquire fence after it orders the caller's later reads (an acquire load
-// per poll would invalidate the caches on every iteration).
-// Once an exchange has timed out (sticky ERROR word set), later waits give
-// up at once: a dead or diverged peer costs ONE timeout, not one per step
-// (the host reports the error at its next check and the data is invalid
-// anyway).
+// Spin until *p >= v (devsync.hpp), then one system acquire that orders the
+// caller's later reads.
 __device__ bool wait_geq(const uint64_t* p, uint64_t v, const PutSync& s, uint64_t code) {
-  const long long t0 = wall_clock64();
-  while (load_sys_relaxed(p) < v) {
-    __builtin_amdgcn_s_sleep(2);
-    if (load_sys_relaxed(s.my_flags + PutFlags::ERROR) != 0) return false;
-    if (wall_clock64() - t0 > s.timeout_ticks) {
-      uint64_t expected = 0;
-      __hip_atomic_compare_exchange_strong(s.my_flags + PutFlags::ERROR, &expected, code, __ATOMIC_RELAXED,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
-    }
-  }
+  if (!spin_geq(p, v, s.my_flags, s.timeout_ticks, code)) return false;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   return true;
 }
@@ -106,6 +82,30 @@ void launch_put_sync(const PutSync& s, hipStream_t stream) {
   if (s.n_out > 64 || s.n_in > 64) fail("launch_put_sync: too many peers");
   hipLaunchKernelGGL(put_sync_kernel, dim3(1), dim3(64), 0, stream, s);
   IGG_HIP_CHECK(hipGetLastError());
+}
+
+StepSync step_sync_from(const PutSync& p) {
+  if (p.n_in != p.n_out) fail("step_sync_from: asymmetric neighbourhood (", p.n_in, " senders, ", p.n_out, " receivers)");
+  if (p.n_in < 1 || p.n_in > STEP_SYNC_MAX_PEERS) fail("step_sync_from: 1..", STEP_SYNC_MAX_PEERS, " peers expected, got ", p.n_in);
+  StepSync s;
+  s.my_flags = p.my_flags;
+  s.n_peers = p.n_in;
+  for (int i = 0; i < p.n_in; ++i) {
+    if (p.in_rank[i] != p.out_rank[i]) fail("step_sync_from: sender and receiver lists differ");
+    s.peer_flags[i] = p.out_flags[i];
+    s.peer_rank[i] = p.in_rank[i];
+  }
+  s.my_rank = p.my_rank;
+  s.timeout_ticks = p.timeout_ticks;
+  return s;
+}
+
+bool step_sync_in_kernel(bool shares_device) {
+  static const int mode = [] {  // -1 auto, 0 in the kernel, 1 sync kernel
+    const char* e = std::getenv("IGG_FUSED_SYNC_KERNEL");
+    return (e && e[0] == '1') ? 1 : ((e && e[0] == '0') ? 0 : -1);
+  }();
+  return mode == 0 || (mode < 0 && !shares_device);
 }
 
 int64_t put_timeout_ticks(double seconds) {

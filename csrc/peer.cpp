@@ -11,6 +11,8 @@
 #include <ios>
 #include <map>
 
+#include <unistd.h>
+
 namespace igg {
 
 PeerMesh::PeerMesh(int rank, int nranks, AllGather allgather)
@@ -25,6 +27,18 @@ PeerMesh::PeerMesh(int rank, int nranks, AllGather allgather)
   timeout_ticks_ = put_timeout_ticks(seconds);
   if (const char* k = std::getenv("IGG_PUT_ARENA_KIND")) arena_kind_ = static_cast<MemKind>(std::atoi(k));
   exchange_handles(true);
+  {
+    // Device identity: host name + PCI bus id of the current device.
+    int dev = 0;
+    char bus[64] = {0}, host[256] = {0};
+    IGG_HIP_CHECK(hipGetDevice(&dev));
+    IGG_HIP_CHECK(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, dev));
+    (void)gethostname(host, sizeof(host) - 1);
+    const std::string id = std::string(host) + "/" + bus;
+    const std::vector<std::string> ids = allgather_(id);
+    for (int r = 0; r < static_cast<int>(ids.size()); ++r)
+      if (r != rank_ && ids[r] == id) shares_device_ = true;
+  }
   if (const char* m = std::getenv("IGG_PUT_ARENA_MIN")) {
     const long long mb = std::atoll(m);
     if (mb > 0) ensure_arena(static_cast<size_t>(mb) << 20);  // collective

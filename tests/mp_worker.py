@@ -366,6 +366,49 @@ def scenario_acoustic_fused_soak(nx, ny, steps, periodic, graph):
     print(f"rank {me} acoustic fused soak OK", flush=True)
 
 
+def scenario_acoustic_fused_skew(nx, ny, rounds, per_round, periodic):
+    """Fused acoustic steps under random host skew (a rank enqueues late, so
+    its neighbours' exchanging waves wait inside their kernels for its previous
+    step), graph replays with odd and even counts, one restore-like write with
+    mark_modified; bitwise vs the update_halo_ path at the end."""
+    import random
+    import time
+
+    from igg.models.acoustic2d import Acoustic2D
+
+    _device("gpu")
+    nx, ny, rounds, per_round, per = int(nx), int(ny), int(rounds), int(per_round), int(periodic)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, 1, periodx=per, periody=per, quiet=True,
+                                                          select_device=False, device_type="AMDGPU")
+    a, b = Acoustic2D(dtype=torch.float32), Acoustic2D(dtype=torch.float32)
+    assert b.set_fused(True)
+    b.capture(steps=4)
+    total = 1
+    rng = random.Random(99 + me)
+    for k in range(rounds):
+        time.sleep(rng.random() * 0.02)
+        n = per_round + (k % 3)
+        b.run(n)
+        total += n
+        if k == rounds // 2:
+            a.run(total)
+            total = 0
+            torch.cuda.synchronize()
+            for name in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2"):
+                getattr(b, name).copy_(getattr(a, name))
+            b.mark_modified()
+    a.run(total)
+    torch.cuda.synchronize()
+    b.check()
+    for name in ("P", "Vx", "Vy", "P2", "Vx2", "Vy2"):
+        x, y = getattr(a, name), getattr(b, name)
+        if not torch.equal(x, y):
+            raise AssertionError(f"rank {me}: {name} differs at {(x != y).nonzero()[:5].tolist()}")
+    b.close()
+    igg.finalize_global_grid()
+    print(f"rank {me} acoustic fused skew OK")
+
+
 def scenario_gather_async():
     """gather_async_: root pulls every block (IPC + copy engine), the caller
     overlaps other work, wait() reorders; then A may change again."""

@@ -168,7 +168,7 @@ def _same(a, b):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("periods", [(1, 0), (0, 1), (1, 1)])
-@pytest.mark.parametrize("shape", [(64, 48), (37, 520), (9, 16)])
+@pytest.mark.parametrize("shape", [(64, 48), (37, 520), (9, 16), (40, 496)])
 def test_gpu_fused_matches_update_halo(gpu, dtype, periods, shape):
     """Fused exchange (the kernel stores the staggered boundary faces into the
     neighbours' next Vx2/Vy2; here the periodic neighbour is this rank) is
@@ -208,11 +208,40 @@ def test_gpu_fused_loopback_graph_and_switch(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nprocs,per", [(2, 1), (4, 0), (4, 1)])
-def test_gpu_fused_multirank(nprocs, per):
+@pytest.mark.parametrize("nprocs,per,sync_kernel", [(2, 1, 0), (4, 0, 0), (4, 1, 0), (4, 1, 1)])
+def test_gpu_fused_multirank(nprocs, per, sync_kernel):
     """Ranks sharing one GPU (put transport for the update_halo_ reference):
-    fused == update_halo_ bitwise on every rank, incl. graph replays."""
-    env = {"IGG_TRANSPORT": "put", "IGG_PUT_TIMEOUT": "20"}
+    fused == update_halo_ bitwise on every rank, incl. graph replays; step
+    synchronisation inside the fused kernel (default) or by a sync kernel."""
+    env = {"IGG_TRANSPORT": "put", "IGG_PUT_TIMEOUT": "20", "IGG_FUSED_SYNC_KERNEL": str(sync_kernel)}
     if nprocs > 2:
         env["GPU_MAX_HW_QUEUES"] = "1"
     run_ranks(nprocs, "acoustic_fused", "gpu", 40, 36, 12, per, env_extra=env, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sync_kernel", [0, 1])
+def test_gpu_fused_multirank_skew(sync_kernel):
+    """4 ranks on one GPU, random host skew between graph-replayed fused steps:
+    the step synchronisation absorbs the drift; bitwise vs update_halo_."""
+    env = {"IGG_TRANSPORT": "put", "IGG_PUT_TIMEOUT": "20", "IGG_FUSED_SYNC_KERNEL": str(sync_kernel),
+           "GPU_MAX_HW_QUEUES": "1"}
+    run_ranks(4, "acoustic_fused_skew", 40, 36, 12, 9, 1, env_extra=env, timeout=150)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(64, 48), (37, 520), (40, 496), (9, 16)])
+def test_gpu_in_kernel_step_sync_counts_every_step(gpu, shape):
+    """EPOCH advances once per fused step and COUNT returns to 0 (the host's
+    count of exchanging waves matches the kernel's)."""
+    a, b = _fused_pair(shape, (1, 1), torch.float32)
+    assert b._fa.in_kernel_sync
+    e0 = b._fa.flag(0)
+    b.run(5)
+    torch.cuda.synchronize()
+    assert b._fa.flag(0) == e0 + 6 and b._fa.flag(2) == 0  # + the entry barrier
+    a.run(5)
+    torch.cuda.synchronize()
+    assert _same(a, b)
+    b.close()
+    igg.finalize_global_grid(finalize_MPI=False)

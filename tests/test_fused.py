@@ -276,3 +276,28 @@ def test_graph_after_odd_step_counts(gpu):
     b.check()
     assert torch.equal(a.T, b.T) and torch.equal(a.T, c.T)
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,mode", [(0, 0), (0, 1), (40, 8), (42, 4), (42, 12), (50, 1)])
+@pytest.mark.parametrize("periods", [(1, 1, 1), (0, 1, 0), (1, 0, 1)])
+def test_in_kernel_step_sync_counts_every_step(gpu, variant, mode, periods):
+    """The in-kernel step synchronisation advances EPOCH exactly once per step
+    and leaves COUNT at 0: the host's count of exchanging waves equals the
+    number of waves that count themselves (a mismatch would stall a real
+    neighbour). Eager steps and graph replays."""
+    a, b = _pair((26, 37, 136), periods, torch.float64, variant, mode=mode)
+    assert b._fh.in_kernel_sync
+    e0 = b._fh.flag(0)
+    b.run(3)
+    torch.cuda.synchronize()
+    assert b._fh.flag(0) == e0 + 4 and b._fh.flag(2) == 0  # + the entry barrier
+    b.capture(steps=4)
+    b.run(9)
+    b.sync_halo()
+    a.run(12)
+    torch.cuda.synchronize()
+    b.check()
+    assert b._fh.flag(0) == e0 + 4 + 9 and b._fh.flag(2) == 0
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)

@@ -141,6 +141,22 @@ def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 1, 0), ("0", "0")),
+                                               (4, (20, 22, 32, 5, 1, 1), ("0", "1")),
+                                               (8, (18, 20, 40, 7, 1, 0), ("0", "5"))])
+def test_diffusion_gpu_multirank_fused_in_kernel_sync(nprocs, cfg, kernel):
+    """The step synchronisation inside the fused kernel across processes
+    (forced: ranks sharing one GPU default to the sync kernel, because waiting
+    waves could hold the compute units another rank's kernel needs; tiling 0
+    leaves room). Bitwise vs stencil + update_halo_."""
+    env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1],
+           "IGG_FUSED_SYNC_KERNEL": "0"}
+    if nprocs > 2:
+        env["GPU_MAX_HW_QUEUES"] = "1"
+    run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=170)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nprocs,kernel", [(4, ("0", "0")), (8, ("0", "1")), (8, ("40", "4"))])
 def test_fused_soak_with_rank_skew(nprocs, kernel):
     """Thousands of graph-replayed fused steps with random host skew between
