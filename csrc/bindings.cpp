@@ -563,6 +563,8 @@ PYBIND11_MODULE(_igg_native, m) {
            py::arg("p2"), py::arg("vx2"), py::arg("vy2"), py::arg("p"), py::arg("vx"), py::arg("vy"), py::arg("nx"),
            py::arg("ny"), py::arg("dtk"), py::arg("dt_rho"), py::arg("rdx"), py::arg("rdy"), py::arg("elem_bytes"),
            py::arg("stream"), py::arg("entry") = false)
+      .def("drain", [](FusedAcoustic& f, uintptr_t s) { f.drain(as_stream(s)); }, py::arg("stream"),
+           "Exit barrier after in-kernel synchronised steps (collective; no-op after a sync-kernel step).")
       .def("check_error", &FusedAcoustic::check_error)
       .def("set_step_sync", &FusedAcoustic::set_step_sync, py::arg("mode"),
            "Step synchronisation: -1 default, 0 inside the fused kernel, 1 sync kernel (same on every rank).")
@@ -634,6 +636,8 @@ PYBIND11_MODULE(_igg_native, m) {
            py::arg("step"), py::arg("primed"), py::arg("stream"), py::arg("rounds") = 0, py::arg("mode") = 0,
            py::arg("entry") = false)
       .def("sync", [](FusedHalo& f, uintptr_t s) { f.sync(as_stream(s)); })
+      .def("drain", [](FusedHalo& f, uintptr_t s) { f.drain(as_stream(s)); }, py::arg("stream"),
+           "Exit barrier after in-kernel synchronised steps (collective; no-op after a sync-kernel step).")
       .def("set_fields", &FusedHalo::set_fields, py::arg("a"), py::arg("b"))
       .def_property_readonly("has_fields", &FusedHalo::has_fields)
       .def("io", [](FusedHalo& f, int64_t step, bool primed, uintptr_t t2, bool direct_z) {

@@ -18,6 +18,10 @@ FusedHalo::FusedHalo(std::shared_ptr<PeerMesh> mesh, const std::array<int64_t, 3
     if (n[d] < 3) fail("FusedHalo: every local extent must be >= 3");
   // Region sizes (elements): dim-0 faces [n1][n2], dim-1 [n0][n2], dim-2
   // [n0][zp] with zp >= n1-2 rounded to 16 (vector stores of up to 16 rows).
+  // The x/y send planes are stored through buffer descriptors with 32-bit
+  // byte offsets (st_sys_at, sysstore.hpp).
+  if (std::max(n[1] * n[2], n[0] * n[2]) * elem_bytes >= (int64_t{1} << 31))
+    fail("FusedHalo: a face of the local grid exceeds 2 GiB");
   zp_ = round_up(n[1] - 2, 16);
   const int64_t sz[3] = {n[1] * n[2], n[0] * n[2], n[0] * zp_};
   const int64_t g = static_cast<int64_t>(DEVICE_ALIGN) / elem_bytes;
@@ -113,9 +117,15 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
   }
   launch_diffusion3d_fused(a, x, variant, mode, stream);
   if (!used) sync(stream);
+  open_ = used;
 }
 
 void FusedHalo::sync(hipStream_t stream) const { launch_put_sync(sync_, stream); }
+
+void FusedHalo::drain(hipStream_t stream) {
+  if (open_) sync(stream);
+  open_ = false;
+}
 
 bool FusedHalo::in_kernel_sync() const {
   return sync_mode_ < 0 ? step_sync_in_kernel(mesh_->shares_device()) : sync_mode_ == 0;

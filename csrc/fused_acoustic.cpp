@@ -82,6 +82,12 @@ void FusedAcoustic::step(const AcousticArgs& a, hipStream_t stream, bool entry) 
   if (entry) launch_put_sync(sync_, stream);  // entry barrier
   launch_acoustic2d_fused(a, h, stream);
   if (sync_kernel) launch_put_sync(sync_, stream);
+  open_ = !sync_kernel;
+}
+
+void FusedAcoustic::drain(hipStream_t stream) {
+  if (open_) launch_put_sync(sync_, stream);
+  open_ = false;
 }
 
 void FusedAcoustic::check_error() const { mesh_->check_error(); }
@@ -89,7 +95,7 @@ void FusedAcoustic::check_error() const { mesh_->check_error(); }
 uint64_t FusedAcoustic::flag(int index) const { return mesh_->read_flag(index); }
 
 bool FusedAcoustic::in_kernel_sync() const {
-  return sync_mode_ < 0 ? step_sync_in_kernel(mesh_->shares_device()) : sync_mode_ == 0;
+  return sync_mode_ < 0 ? step_sync_in_kernel(mesh_->shares_device(), false) : sync_mode_ == 0;
 }
 
 void FusedAcoustic::close() {

@@ -86,6 +86,9 @@ class FusedAcoustic {
   // `entry`: a sync kernel first (a neighbour's remote stores must not
   // overtake this rank's own earlier writes to the fields: FusedHalo::step).
   void step(const AcousticArgs& a, hipStream_t stream, bool entry = false);
+  // Exit barrier after in-kernel synchronised steps (FusedHalo::drain):
+  // collective, a sync kernel only if the last step left remote stores open.
+  void drain(hipStream_t stream);
   void check_error() const;
   uint64_t flag(int index) const;  // own flag word (PutFlags), host read
   // Step synchronisation form (FusedHalo::set_step_sync).
@@ -100,6 +103,7 @@ class FusedAcoustic {
   std::array<std::array<int, 2>, 2> nb_;
   PutSync sync_{};
   int sync_mode_ = -1;
+  bool open_ = false;  // the last step synchronised inside the kernel (drain() pending)
   std::vector<std::vector<char*>> fields_;  // [rank][vx_a, vx_b, vy_a, vy_b]
 };
 

@@ -57,7 +57,9 @@ __device__ inline uint64_t step_sync_enter(const StepSync& s, int lane) {
   const uint64_t c = load_sys_relaxed(s.my_flags + PutFlags::EPOCH);
   if (lane < s.n_peers)
     spin_geq(s.my_flags + PutFlags::ARRIVED + s.peer_rank[lane], c, s.my_flags, s.timeout_ticks, 0x300 + lane);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (s.acquire >= 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  else if (s.acquire == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   return c;
 }
 

@@ -79,6 +79,14 @@ class FusedHalo {
   }
   // Only the sync kernel (e.g. to rehearse the barrier cost).
   void sync(hipStream_t stream) const;
+  // Exit barrier: after steps synchronised inside the kernel, the last step's
+  // remote stores into THIS rank's arena and fields are complete only once
+  // every neighbour has finished that step - nothing on this rank waits for
+  // that until the neighbours' next step. drain() launches the sync kernel if
+  // the last step() left such stores open (none after a sync-kernel step), so
+  // work queued behind it (a restore, a comparison, gather, another exchange)
+  // sees the fields final. Collective: every rank drains at the same step.
+  void drain(hipStream_t stream);
   // Step synchronisation inside the fused kernel (put.hpp StepSync) or by the
   // sync kernel after it: -1 the default (step_sync_in_kernel), 0 in the
   // kernel, 1 sync kernel. Every rank must use the same form.
@@ -104,6 +112,7 @@ class FusedHalo {
   int64_t half_ = 0, zp_ = 0;
   PutSync sync_{};
   int sync_mode_ = -1;
+  bool open_ = false;  // the last step synchronised inside the kernel (drain() pending)
   std::vector<std::vector<char*>> fields_;  // [rank][k]: ping-pong buffer k (set_fields)
 };
 

@@ -416,16 +416,16 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         }
         // Send planes / rows (whole vectors of the lanes that own them: the
         // halo elements they carry are never read by the receiver).
-        if (xd0 && zown) st_sys(reinterpret_cast<V*>(xd0 + rowb[r] + zl), out);
-        if (xd1 && zown) st_sys(reinterpret_cast<V*>(xd1 + rowb[r] + zl), out);
+        if (xd0 && zown) st_sys_at(xd0, static_cast<uint32_t>((rowb[r] + zl) * sizeof(T)), out);
+        if (xd1 && zown) st_sys_at(xd1, static_cast<uint32_t>((rowb[r] + zl) * sizeof(T)), out);
         if (r == 0 && yrow0) {
           if (DF) { ysend = out; ysend_dst = zown ? yrow0 + x * n2 + zl : nullptr; }
-          else if (zown) st_sys(reinterpret_cast<V*>(yrow0 + x * n2 + zl), out);
+          else if (zown) st_sys_at(yrow0, static_cast<uint32_t>((x * n2 + zl) * sizeof(T)), out);
         }
         if (r == ry1) {
           // one deferral slot: taken by row 0 if this wave also sends that row
           if (DF && !yrow0) { ysend = out; ysend_dst = zown ? yrow1 + x * n2 + zl : nullptr; }
-          else if (zown) st_sys(reinterpret_cast<V*>(yrow1 + x * n2 + zl), out);
+          else if (zown) st_sys_at(yrow1, static_cast<uint32_t>((x * n2 + zl) * sizeof(T)), out);
         }
         if constexpr (ZE && (FEAT & 8) != 0) {
           zo_buf[r] = has_lo ? out[1] : out[VZ - 2];  // the send element of the edge lane

@@ -68,15 +68,22 @@ struct StepSync {
   int n_peers = 0, my_rank = 0;
   int64_t timeout_ticks = 0;
   int64_t feat_waves = 0;  // exchanging waves of the launch (set by the launcher)
+  // Acquire after the wait (measurement knob IGG_STEP_SYNC_ACQUIRE): 2 system
+  // (buffer_inv sc0 sc1, the default), 1 agent (buffer_inv sc1), 0 workgroup
+  // (compiler ordering only; the kernel start invalidated the L1).
+  int acquire = 2;
 };
 // The StepSync of a face-neighbour PutSync (every peer both sends and receives).
 StepSync step_sync_from(const PutSync& s);
 // Whether a fused exchange synchronises its steps inside the step kernel.
-// IGG_FUSED_SYNC_KERNEL unset: yes unless another rank of the mesh shares
-// this rank's GPU (its waiting waves could starve that rank's kernel); "1":
-// never (the sync kernel after every step); "0": always (tests whose kernels
-// cannot fill the GPU).
-bool step_sync_in_kernel(bool shares_device);
+// IGG_FUSED_SYNC_KERNEL unset: `by_default` unless another rank of the mesh
+// shares this rank's GPU (its waiting waves could starve that rank's kernel);
+// "1": never (the sync kernel after every step); "0": always (tests whose
+// kernels cannot fill the GPU). FusedHalo passes by_default = true; the
+// acoustic step false: its ~8,300 exchanging waves per 8192^2 step each count
+// themselves with one atomic on the same uncached word, and those serialise
+// (0.70-0.75 vs 0.306 ms/step with the sync kernel, profiles/r3_stepsync/).
+bool step_sync_in_kernel(bool shares_device, bool by_default = true);
 
 void launch_put_begin(const PutSync& s, hipStream_t stream);
 void launch_put_sync(const PutSync& s, hipStream_t stream);

@@ -50,4 +50,28 @@ __device__ __forceinline__ void st_sys(V* p, const V& v) {
   }
 }
 
+// A 16- or 32-B vector at `base` + `off` bytes as `buffer_store_dwordx4 ...
+// sc0 sc1` (one or two): the same write-through system-scope store as st_sys,
+// without splitting the vector into 8-B atomic stores (a `sc0 sc1` store is
+// one fabric write each: dwordx2 costs 2.7x a dwordx4 per byte,
+// MI355X_MICROARCH.md). A compiler builtin, so its hazards are tracked like
+// any other store (unlike rounds 2-3's inline asm). `base` must be
+// wave-uniform (it becomes the buffer descriptor in SGPRs) and `off` < 2 GiB.
+template <typename V>
+__device__ __forceinline__ void st_sys_at(const void* base, uint32_t off, const V& v) {
+  if constexpr (sizeof(V) == 16 || sizeof(V) == 32) {
+    typedef unsigned int U4 __attribute__((ext_vector_type(4)));
+    struct W { U4 q[sizeof(V) / 16]; };
+    const W x = __builtin_bit_cast(W, v);
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), static_cast<short>(0), 0x7fffffff, 0x00020000);
+    constexpr int SC0_SC1 = 1 | 16;  // cache policy bits of the gfx94x/gfx950 encoding
+#pragma unroll
+    for (int i = 0; i < static_cast<int>(sizeof(V) / 16); ++i)
+      __builtin_amdgcn_raw_buffer_store_b128(x.q[i], r, static_cast<int>(off) + 16 * i, 0, SC0_SC1);
+  } else {
+    st_sys(reinterpret_cast<V*>(static_cast<char*>(const_cast<void*>(base)) + off), v);
+  }
+}
+
 }  // namespace igg

@@ -97,15 +97,20 @@ StepSync step_sync_from(const PutSync& p) {
   }
   s.my_rank = p.my_rank;
   s.timeout_ticks = p.timeout_ticks;
+  static const int acq = [] {
+    const char* e = std::getenv("IGG_STEP_SYNC_ACQUIRE");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
+  }();
+  s.acquire = acq;
   return s;
 }
 
-bool step_sync_in_kernel(bool shares_device) {
+bool step_sync_in_kernel(bool shares_device, bool by_default) {
   static const int mode = [] {  // -1 auto, 0 in the kernel, 1 sync kernel
     const char* e = std::getenv("IGG_FUSED_SYNC_KERNEL");
     return (e && e[0] == '1') ? 1 : ((e && e[0] == '0') ? 0 : -1);
   }();
-  return mode == 0 || (mode < 0 && !shares_device);
+  return mode == 0 || (mode < 0 && by_default && !shares_device);
 }
 
 int64_t put_timeout_ticks(double seconds) {

@@ -157,6 +157,21 @@ class Acoustic2D:
             self.graph = None
 
     def step(self) -> None:
+        """Advance one time step. In fused mode the fields are final when the
+        call returns (as far as stream order goes): the neighbours' stores of
+        this step into them precede later work on the stream (``_drain``)."""
+        self._step()
+        self._drain()
+
+    def _drain(self) -> None:
+        """Exit barrier of in-kernel synchronised fused steps (collective): the
+        last step's neighbour stores into this rank's fields are complete before
+        anything queued after it (a restore, a comparison, gather_, a mode
+        switch) touches the fields. No-op after a sync-kernel step."""
+        if self.fused:
+            self._fa.drain(torch.cuda.current_stream().cuda_stream)
+
+    def _step(self) -> None:
         if self.fused:
             s = torch.cuda.current_stream().cuda_stream
             self._fa.step(self.P2.data_ptr(), self.Vx2.data_ptr(), self.Vy2.data_ptr(), self.P.data_ptr(),
@@ -186,7 +201,7 @@ class Acoustic2D:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for _ in range(steps):
-                self.step()
+                self._step()  # no exit barrier inside the graph: run() drains once
         torch.cuda.synchronize()
         register_graph(g)
         self.graph = g
@@ -194,18 +209,23 @@ class Acoustic2D:
         self._graph_P = self.P.data_ptr()
 
     def run(self, nt: int) -> None:
+        """Advance ``nt`` steps (graph replays where captured); one exit barrier
+        at the end in fused mode (``_drain``), none between the steps."""
+        ran = nt > 0
         if self.graph is not None:
             # The captured steps read the capture's P/Vx/Vy first and hold no
             # entry barrier: one eager step realigns an odd step count or
             # performs a pending barrier (mark_modified, restore).
             while nt > 0 and not self._graph_ready():
-                self.step()
+                self._step()
                 nt -= 1
             for _ in range(nt // self.graph_steps):
                 self.graph.replay()
             nt %= self.graph_steps
         for _ in range(nt):
-            self.step()
+            self._step()
+        if ran:
+            self._drain()
 
     def _graph_ready(self) -> bool:
         return self.P.data_ptr() == self._graph_P and not (self.fused and self._entry)

@@ -290,7 +290,21 @@ class Diffusion3D:
                     rounds=self.rounds if rounds is None else rounds)
 
     def step(self) -> None:
-        """Advance one time step (T <- T2 after the update and halo exchange)."""
+        """Advance one time step (T <- T2 after the update and halo exchange).
+        In fused mode the neighbours' stores of this step into this rank's
+        arena and fields precede later work on the stream (``_drain``)."""
+        self._step()
+        self._drain()
+
+    def _drain(self) -> None:
+        """Exit barrier of in-kernel synchronised fused steps (collective): the
+        last step's neighbour stores (arena, direct-z halo column) are complete
+        before anything queued after it touches them (sync_halo, a restore, a
+        comparison, gather_). No-op after a sync-kernel step."""
+        if self.fused:
+            self._fh.drain(torch.cuda.current_stream().cuda_stream)
+
+    def _step(self) -> None:
         T, T2, Cp = self.T, self.T2, self.Cp
         if self.fused:
             rd2 = [1.0 / self.dx ** 2, 1.0 / self.dy ** 2, 1.0 / self.dz ** 2]
@@ -378,7 +392,7 @@ class Diffusion3D:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for _ in range(steps):
-                self.step()
+                self._step()  # no exit barrier inside the graph: run() drains once
         torch.cuda.synchronize()
         register_graph(g)
         self.graph = g
@@ -388,7 +402,9 @@ class Diffusion3D:
         self._graph_T = self.T.data_ptr()
 
     def run(self, nt: int) -> None:
-        """Advance ``nt`` steps (by graph replays of ``graph_steps`` steps if captured)."""
+        """Advance ``nt`` steps (by graph replays of ``graph_steps`` steps if
+        captured); in fused mode one exit barrier at the end (``_drain``)."""
+        ran = nt > 0
         if self.graph is not None and self._graph_fused == self.fused:
             # The captured steps have their buffer roles baked in (T of the
             # capture is read first) and, fused, their arena halves too: they
@@ -399,7 +415,7 @@ class Diffusion3D:
             for _ in range(2):
                 if nt == 0 or self._graph_ready():
                     break
-                self.step()
+                self._step()
                 nt -= 1
             if self._graph_ready():
                 k = self.graph_steps
@@ -409,7 +425,9 @@ class Diffusion3D:
                     self._fstep += k * (nt // k)
                 nt %= k
         for _ in range(nt):
-            self.step()
+            self._step()
+        if ran:
+            self._drain()
 
     def _graph_ready(self) -> bool:
         if self.T.data_ptr() != self._graph_T:

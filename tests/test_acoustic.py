@@ -235,11 +235,14 @@ def test_gpu_in_kernel_step_sync_counts_every_step(gpu, shape):
     """EPOCH advances once per fused step and COUNT returns to 0 (the host's
     count of exchanging waves matches the kernel's)."""
     a, b = _fused_pair(shape, (1, 1), torch.float32)
+    assert not b._fa.in_kernel_sync  # the acoustic default: the sync kernel (put.hpp)
+    b._fa.set_step_sync(0)
     assert b._fa.in_kernel_sync
     e0 = b._fa.flag(0)
     b.run(5)
     torch.cuda.synchronize()
-    assert b._fa.flag(0) == e0 + 6 and b._fa.flag(2) == 0  # + the entry barrier
+    # + the entry barrier and run()'s exit barrier (drain)
+    assert b._fa.flag(0) == e0 + 7 and b._fa.flag(2) == 0
     a.run(5)
     torch.cuda.synchronize()
     assert _same(a, b)

@@ -291,13 +291,14 @@ def test_in_kernel_step_sync_counts_every_step(gpu, variant, mode, periods):
     e0 = b._fh.flag(0)
     b.run(3)
     torch.cuda.synchronize()
-    assert b._fh.flag(0) == e0 + 4 and b._fh.flag(2) == 0  # + the entry barrier
+    # + the entry barrier and run()'s exit barrier (drain)
+    assert b._fh.flag(0) == e0 + 5 and b._fh.flag(2) == 0
     b.capture(steps=4)
     b.run(9)
     b.sync_halo()
     a.run(12)
     torch.cuda.synchronize()
     b.check()
-    assert b._fh.flag(0) == e0 + 4 + 9 and b._fh.flag(2) == 0
+    assert b._fh.flag(0) == e0 + 5 + 9 + 1 and b._fh.flag(2) == 0
     assert torch.equal(a.T, b.T)
     igg.finalize_global_grid(finalize_MPI=False)
