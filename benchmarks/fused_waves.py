@@ -49,7 +49,10 @@ def main():
     inner = [([1, 1, 1], [n - 1, n - 1, n - 1])]
     mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
     fh6 = native.FusedHalo(mesh, [n, n, n], eb, [[0, 0], [0, 0], [0, 0]])
-    fh0 = native.FusedHalo(mesh, [n, n, n], eb, [[-1, -1], [-1, -1], [-1, -1]])
+    # its own mesh: a neighbourless halo advances EPOCH without publishing
+    # ARRIVED, which would stall fh6's in-kernel step sync on a shared flag block
+    fh0 = native.FusedHalo(native.PeerMesh(0, 1, lambda b: [bytes(b)]), [n, n, n], eb,
+                           [[-1, -1], [-1, -1], [-1, -1]])
     if a.mode & 4:  # direct z: the z sends land in the halo column of the other buffer
         fh6.set_fields(T.data_ptr(), T2.data_ptr())
     stamps = torch.zeros(1 << 22, dtype=torch.int64, device="cuda")

@@ -111,7 +111,7 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
   // kernel after it (IGG_FUSED_SYNC_KERNEL=1, or a launch that cannot count
   // its exchanging waves).
   bool used = false;
-  if (in_kernel_sync()) {
+  if (in_kernel_sync() && sync_.n_out > 0) {  // no neighbour: nothing to synchronise in the kernel
     x.sync = step_sync_from(sync_);
     x.sync_used = &used;
   }
