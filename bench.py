@@ -628,6 +628,10 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
 
 def main():
     args = parse()
+    if os.environ.get("IGG_BENCH_STACKS"):  # diagnosis of a hang: every rank's Python stack every N s
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["IGG_BENCH_STACKS"]), repeat=True)
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         sys.exit(self_launch(args))

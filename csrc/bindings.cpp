@@ -257,6 +257,9 @@ PYBIND11_MODULE(_igg_native, m) {
   m.def("alloc_dlpack", &alloc_dlpack, py::arg("bytes"), py::arg("kind"),
         "Zeroed device allocation of a MemKind as a DLPack capsule (1-D uint8; torch.utils.dlpack.from_dlpack).");
   m.def("ipc_get_handle", [](uintptr_t p) { return py::bytes(ipc_get_handle(reinterpret_cast<void*>(p))); });
+  m.def("alloc_bytes", [](uintptr_t p) { return alloc_bytes(reinterpret_cast<const void*>(p)); }, py::arg("ptr"),
+        "Size of the device allocation holding `ptr` (hipMemGetAddressRange).");
+  m.attr("IPC_MAX_BYTES") = py::int_(IPC_MAX_BYTES);
   m.def("ipc_open", [](const std::string& h) { return reinterpret_cast<uintptr_t>(ipc_open(h)); });
   m.def("ipc_close", [](uintptr_t p) { ipc_close(reinterpret_cast<void*>(p)); });
   m.def("stream_write_u64", [](uintptr_t s, uintptr_t p, uint64_t v) {

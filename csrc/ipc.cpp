@@ -24,7 +24,17 @@ void ipc_free(void* p) {
   IGG_HIP_CHECK(hipFree(p));
 }
 
+size_t alloc_bytes(const void* p) {
+  void* base = nullptr;
+  size_t size = 0;
+  IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)));
+  return size;
+}
+
 std::string ipc_get_handle(void* p) {
+  if (const size_t n = alloc_bytes(p); n >= IPC_MAX_BYTES)
+    fail("IPC export of a ", n >> 20, " MiB allocation refused: opening IPC handles of allocations of 2 GiB or "
+         "more hangs on this ROCm runtime (profiles/r3_ipc/)");
   hipIpcMemHandle_t h;
   IGG_HIP_CHECK(hipIpcGetMemHandle(&h, p));
   return std::string(reinterpret_cast<const char*>(&h), sizeof(h));

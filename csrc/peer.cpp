@@ -130,7 +130,10 @@ void PeerMesh::ensure_arena(size_t bytes) {
     const long long mb = f ? std::atoll(f) : 64;
     return static_cast<size_t>(mb > 0 ? mb : 1) << 20;
   }();
+  if (bytes >= IPC_MAX_BYTES)  // every rank computes the same size: all fail together
+    fail("PeerMesh: a receive arena of ", bytes >> 20, " MiB exceeds the 2 GiB IPC limit (ipc.hpp IPC_MAX_BYTES)");
   bytes = static_cast<size_t>(round_up(static_cast<int64_t>(std::max({bytes, 2 * arena_bytes_, floor_bytes})), 1 << 20));
+  bytes = std::min(bytes, IPC_MAX_BYTES - (size_t{1} << 20));  // geometric growth stays exportable
   // Every rank drains its own puts/unpacks into the old arenas, then agrees
   // (allgather = barrier) before anyone unmaps them.
   IGG_HIP_CHECK(hipDeviceSynchronize());

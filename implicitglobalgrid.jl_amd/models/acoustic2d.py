@@ -69,7 +69,7 @@ class Acoustic2D:
         if self.device.type == "cuda" and _os.environ.get("IGG_FIELD_MEMORY", "fine") != "torch":
             # One fine-grained allocation (the fused exchange stores into the
             # neighbours' Vx2/Vy2 while their kernels run: docs/COHERENCE.md).
-            fields = _carve_fine(fields)
+            fields = _carve_fine(fields, split=int(gg.nprocs) > 1)
         self.P, self.Vx, self.Vy, self.P2, self.Vx2, self.Vy2 = fields
         # P's halo cells, evaluated from the global coordinates above, equal
         # the neighbours' cells only up to rounding (periodic wrap of x_g);
@@ -258,16 +258,20 @@ class Acoustic2D:
         return 2 * (self.P.numel() + self.Vx.numel() + self.Vy.numel()) * self.P.element_size()
 
 
-def _carve_fine(tensors):
+def _carve_fine(tensors, split: bool = False):
     """Copies of ``tensors`` carved from one native fine-grained allocation
-    (256 B-aligned slices)."""
-    from .diffusion3d import native_buffer
+    (256 B-aligned slices). ``split``: if that allocation would reach the IPC
+    size limit (the neighbours map the velocity buffers), one allocation per
+    tensor instead."""
+    from .diffusion3d import _ipc_limit, native_buffer
 
     sizes = [t.numel() * t.element_size() for t in tensors]
     offs, pos = [], 0
     for n in sizes:
         offs.append(pos)
         pos += -(-n // 256) * 256
+    if split and pos >= _ipc_limit() and len(tensors) > 1:
+        return [_carve_fine([t])[0] for t in tensors]
     buf = native_buffer(pos, 1, tensors[0].device)
     out = []
     for t, o, n in zip(tensors, offs, sizes):

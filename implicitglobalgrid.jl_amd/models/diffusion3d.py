@@ -117,8 +117,12 @@ class Diffusion3D:
         if self.field_memory not in ("torch", "fine"):
             raise ValueError(f"Diffusion3D: field_memory must be 'torch' or 'fine', got {self.field_memory!r}")
         if self.device.type == "cuda":
+            # With neighbours in other processes T/T2 may be IPC-mapped (direct
+            # z, gather_ pull): no allocation may reach the IPC size limit, so
+            # a carve that would is split into one allocation per array.
             self.T, self.Cp, self.T2 = _carve([self.T, self.Cp, self.T2], gap=266240,
-                                              kind=1 if self.field_memory == "fine" else None)
+                                              kind=1 if self.field_memory == "fine" else None,
+                                              split_at=_ipc_limit() if int(gg.nprocs) > 1 else None)
         sides = [[bool(gg.neighbors[0, d] != -1), bool(gg.neighbors[1, d] != -1)] for d in range(3)]
         self.sides = sides
         self.can_overlap = self.device.type == "cuda" and any(any(sd) for sd in sides)
@@ -456,12 +460,23 @@ def _make_fused_halo(m: "Diffusion3D"):
     return native.FusedHalo(mesh, list(m.T.shape), m.T.element_size(), nb)
 
 
-def _carve(tensors, gap: int, kind=None):
+def _ipc_limit() -> int:
+    """Allocation size from which IPC export is refused (csrc/include/igg/ipc.hpp)."""
+    from .._native import native
+
+    return int(native.IPC_MAX_BYTES)
+
+
+def _carve(tensors, gap: int, kind=None, split_at=None):
     """Copies of equally sized tensors placed in one buffer ``gap`` bytes apart.
     ``kind``: None = torch's caching allocator, else a native MemKind (1 =
-    fine-grained) allocated by the runtime and handed over through DLPack."""
+    fine-grained) allocated by the runtime and handed over through DLPack.
+    ``split_at``: if the one buffer would reach this many bytes, one
+    allocation per tensor instead (the IPC size limit)."""
     nbytes = tensors[0].numel() * tensors[0].element_size()
     stride = nbytes + gap
+    if split_at is not None and stride * len(tensors) >= split_at and len(tensors) > 1:
+        return [_carve([t], 0, kind)[0] for t in tensors]
     if kind is None:
         buf = torch.empty(stride * len(tensors), dtype=torch.uint8, device=tensors[0].device)
     else:

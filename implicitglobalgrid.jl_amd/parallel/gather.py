@@ -8,7 +8,8 @@ gathered into a 3-D ``A_global``); ``A_global`` may be ``None`` off-root; the
 root keeps a grow-only internal buffer until ``finalize_global_grid``.
 
 MI355X paths (csrc/gather.cpp):
-* GPU ``A``, all ranks on one node (the default; IGG_GATHER_PULL=0 disables):
+* GPU ``A``, all ranks on one node, allocations below the IPC size limit
+  (the default; IGG_GATHER_PULL=0 disables):
   the root's copy engines pull every block over xGMI straight into its place
   in ``A_global`` (one 3-D peer copy per block, up to 8 concurrent copy
   streams, ordered by interprocess events): no staging buffer of
@@ -50,11 +51,18 @@ def free_gather_buffer() -> None:
     _sync_puller = None
 
 
-def _pull_ok(gg) -> bool:
-    """Pull path for GPU fields: every rank on this node (IPC-mappable peers).
-    The same answer on every rank (the choice is collective)."""
+def _pull_ok(gg, A: torch.Tensor) -> bool:
+    """Pull path for GPU fields: every rank on this node (IPC-mappable peers)
+    and every rank's allocation holding ``A`` below the IPC size limit
+    (``native.IPC_MAX_BYTES``: opening a larger handle hangs on this ROCm
+    runtime, csrc/include/igg/ipc.hpp). Collective (one gloo all-reduce); the
+    same answer on every rank."""
     c = gg.comm
-    return int(gg.nprocs) > 1 and c is not None and c.local_size == c.size and config.gather_pull()
+    if not (int(gg.nprocs) > 1 and c is not None and c.local_size == c.size and config.gather_pull()):
+        return False
+    t = torch.tensor([float(native.alloc_bytes(A.data_ptr()))], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=c.gloo)
+    return float(t.item()) < float(native.IPC_MAX_BYTES)
 
 
 def _padded_shape(A: torch.Tensor) -> list[int]:
@@ -83,9 +91,11 @@ def gather_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) ->
         if A_global.dtype != A.dtype:
             raise IGGError("The input arguments A and A_global must have the same element type.")
     s = _padded_shape(A)
-    if A.is_cuda and gg.amdgpu_enabled and _pull_ok(gg):
-        _gather_pull(A, A_global, root, s, dims, me, nprocs, c)
-        return
+    if A.is_cuda and gg.amdgpu_enabled:
+        A = A.contiguous()
+        if _pull_ok(gg, A):
+            _gather_pull(A, A_global, root, s, dims, me, nprocs, c)
+            return
     if A.is_cuda and nprocs > 1 and c.rccl is None and gg.amdgpu_enabled and config.transport_choice() == "rccl":
         c.ensure_rccl()
     if A.is_cuda and (nprocs == 1 or c.rccl is not None):
@@ -190,7 +200,9 @@ def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int =
     global _puller
     gg = _grid.global_grid()
     nprocs, me = int(gg.nprocs), int(gg.me)
-    if not (A.is_cuda and nprocs > 1):
+    if not (A.is_cuda and nprocs > 1) or not _pull_ok(gg, A):
+        # one process, or not IPC-mappable (another node, or an allocation
+        # above the IPC size limit): the synchronous gather_ (RCCL / host)
         gather_(A, A_global, root=root)
         return GatherHandle(A_global, True)
     if me == root:
