@@ -30,7 +30,23 @@ def run_ranks(nprocs: int, scenario: str, *args, timeout: float = 150.0, env_ext
     """Run ``scenario`` on ``nprocs`` ranks. Fail-fast: the first rank that
     exits non-zero stops the others (a dead rank would otherwise leave its
     peers blocked in a collective until the timeout); on a timeout every
-    rank's output tail is reported."""
+    rank's output tail is reported. A rendezvous whose port was taken between
+    free_port() and rank 0's listen (EADDRINUSE: nothing ran yet) is retried
+    on a new port, twice at most."""
+    for attempt in range(3):
+        try:
+            return _run_ranks_once(nprocs, scenario, *args, timeout=timeout, env_extra=env_extra)
+        except _PortTaken:
+            if attempt == 2:
+                raise AssertionError(f"scenario {scenario}: rendezvous port taken three times (EADDRINUSE)")
+    raise AssertionError("unreachable")
+
+
+class _PortTaken(Exception):
+    pass
+
+
+def _run_ranks_once(nprocs: int, scenario: str, *args, timeout: float, env_extra) -> list[str]:
     timeout = min(timeout, MAX_TIMEOUT)
     port = free_port()
     procs, logs = [], []
@@ -73,6 +89,8 @@ def run_ranks(nprocs: int, scenario: str, *args, timeout: float = 150.0, env_ext
         log.close()
     codes = [p.returncode for p in procs]
     if first_bad is not None:
+        if "EADDRINUSE" in outs[first_bad] and "init_process_group" in outs[first_bad]:
+            raise _PortTaken()
         raise AssertionError(f"scenario {scenario}: rank {first_bad} failed (rc={codes[first_bad]}), "
                              f"the others were stopped:\n{outs[first_bad][-4000:]}")
     if any(c != 0 for c in codes):
