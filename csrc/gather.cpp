@@ -3,6 +3,8 @@
 #include "igg/trace.hpp"
 #include "igg/ipc.hpp"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include <hip/hip_runtime_api.h>
@@ -55,10 +57,11 @@ namespace {
 
 constexpr int MAX_COPY_STREAMS = 8;
 
-// One 3-D copy of a C-contiguous block of extent s (elements) into its place
-// (block coords c) in the C-contiguous global array of extent dims*s.
-void copy_block(const void* src, void* dst, const Int3& s, const Int3& dims, const Int3& c, int eb,
-                hipStream_t stream) {
+// One 3-D copy of planes [x0, x0 + nx) of a C-contiguous block of extent s
+// (elements; `src` points at plane x0) into their place (block coords c) in the
+// C-contiguous global array of extent dims*s.
+void copy_block(const void* src, void* dst, const Int3& s, const Int3& dims, const Int3& c, int64_t x0, int64_t nx,
+                int eb, hipStream_t stream) {
   const size_t row = static_cast<size_t>(s[2]) * eb;
   hipMemcpy3DParms p{};
   p.srcPtr = make_hipPitchedPtr(const_cast<void*>(src), row, row, static_cast<size_t>(s[1]));
@@ -66,10 +69,29 @@ void copy_block(const void* src, void* dst, const Int3& s, const Int3& dims, con
                                 static_cast<size_t>(dims[1] * s[1]));
   p.srcPos = make_hipPos(0, 0, 0);
   p.dstPos = make_hipPos(static_cast<size_t>(c[2] * s[2]) * eb, static_cast<size_t>(c[1] * s[1]),
-                         static_cast<size_t>(c[0] * s[0]));
-  p.extent = make_hipExtent(row, static_cast<size_t>(s[1]), static_cast<size_t>(s[0]));
+                         static_cast<size_t>(c[0] * s[0] + x0));
+  p.extent = make_hipExtent(row, static_cast<size_t>(s[1]), static_cast<size_t>(nx));
   p.kind = hipMemcpyDeviceToDevice;
   IGG_HIP_CHECK(hipMemcpy3DAsync(&p, stream));
+}
+
+// Staging chunk size for blocks that cannot be exported whole:
+// IGG_GATHER_CHUNK_BYTES (tests: blocks larger than this are staged too),
+// else half the IPC limit.
+size_t chunk_cap(bool* forced) {
+  static const long long b = [] {
+    const char* e = std::getenv("IGG_GATHER_CHUNK_BYTES");
+    return e ? std::atoll(e) : 0LL;
+  }();
+  *forced = b > 0;
+  return b > 0 ? static_cast<size_t>(b) : IPC_MAX_BYTES / 2;
+}
+
+void put_u32(std::string& r, uint32_t v) { r.append(reinterpret_cast<const char*>(&v), 4); }
+uint32_t get_u32(const std::string& r, size_t at) {
+  uint32_t v = 0;
+  std::memcpy(&v, r.data() + at, 4);
+  return v;
 }
 
 }  // namespace
@@ -78,13 +100,16 @@ PullGatherer::PullGatherer(int rank, int nranks, AllGather allgather)
     : rank_(rank), nranks_(nranks), allgather_(std::move(allgather)) {
   peer_key_.assign(nranks, std::string());
   peer_ev_.assign(nranks, nullptr);
-  mapped_.assign(nranks, {std::string(), nullptr});
+  mapped_.assign(nranks, {});
 }
 
 PullGatherer::~PullGatherer() {
   for (hipStream_t s : side_) (void)hipStreamSynchronize(s);
-  for (auto& m : mapped_)
-    if (m.second) (void)hipIpcCloseMemHandle(m.second);
+  for (auto& per : mapped_)
+    for (auto& m : per)
+      if (m.second) (void)hipIpcCloseMemHandle(m.second);
+  if (!stage_.empty()) (void)hipDeviceSynchronize();
+  for (char* c : stage_) (void)hipFree(c);
   for (hipEvent_t& e : peer_ev_)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : root_done_)
@@ -110,10 +135,15 @@ void PullGatherer::ensure_streams() {
 void PullGatherer::free() {
   if (pending_) fail("gather_async: free while a gather is pending (call wait() first)");
   for (hipStream_t s : side_) IGG_HIP_CHECK(hipStreamSynchronize(s));
-  for (auto& m : mapped_) {
-    if (m.second) (void)hipIpcCloseMemHandle(m.second);
-    m = {std::string(), nullptr};
+  for (auto& per : mapped_) {
+    for (auto& m : per)
+      if (m.second) (void)hipIpcCloseMemHandle(m.second);
+    per.clear();
   }
+  if (!stage_.empty()) IGG_HIP_CHECK(hipDeviceSynchronize());
+  for (char* c : stage_) IGG_HIP_CHECK(hipFree(c));
+  stage_.clear();
+  stage_bytes_ = 0;
 }
 
 void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream) {
@@ -125,22 +155,56 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
   if (rank_ == root && !dst) fail("The input argument A_global can't be `nothing` on the root");
   ensure_streams();
   const size_t EH = sizeof(hipIpcEventHandle_t), MH = sizeof(hipIpcMemHandle_t);
-  // `a` (and, on the root, dst) is final where the caller's stream has got to
-  // now: an interprocess event marks that point (no host drain).
-  IGG_HIP_CHECK(hipEventRecord(ready_, stream));
-  hipIpcEventHandle_t eh;
-  IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, ready_));
-  std::string mine(reinterpret_cast<const char*>(&eh), EH);
+  const size_t plane = static_cast<size_t>(a.size[1] * a.size[2]) * a.elem_bytes;
+  std::string rec;  // after the event handle: 'D' handle offset | 'C' nchunks planes/chunk handles...
   if (rank_ != root) {
     void* base = nullptr;
     size_t size = 0;
     IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(a.ptr)));
-    hipIpcMemHandle_t h;
-    IGG_HIP_CHECK(hipIpcGetMemHandle(&h, base));
-    const uint64_t off = a.ptr - reinterpret_cast<uintptr_t>(base);
-    mine.append(reinterpret_cast<const char*>(&h), MH);
-    mine.append(reinterpret_cast<const char*>(&off), sizeof(off));
-  } else {
+    bool forced = false;
+    const size_t cap = chunk_cap(&forced);
+    if (size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
+      // Stage into exportable chunks of whole planes (class comment).
+      const int64_t ppc = std::max<int64_t>(1, static_cast<int64_t>(cap / std::max<size_t>(plane, 1)));
+      const size_t cb = static_cast<size_t>(ppc) * plane;
+      if (cb >= IPC_MAX_BYTES) fail("gather_async: one x-plane of the local array exceeds the IPC limit");
+      const int64_t nch = (a.size[0] + ppc - 1) / ppc;
+      if (stage_bytes_ < cb || static_cast<int64_t>(stage_.size()) < nch) {
+        IGG_HIP_CHECK(hipDeviceSynchronize());  // rare (grow-only): no pull of the old chunks in flight
+        for (char* c : stage_) IGG_HIP_CHECK(hipFree(c));
+        stage_.clear();
+        for (int64_t k = 0; k < nch; ++k) {
+          char* c = nullptr;
+          IGG_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c), cb));
+          stage_.push_back(c);
+        }
+        stage_bytes_ = cb;
+      }
+      rec.push_back('C');
+      put_u32(rec, static_cast<uint32_t>(nch));
+      put_u32(rec, static_cast<uint32_t>(ppc));
+      for (int64_t k = 0; k < nch; ++k) {
+        const int64_t nx = std::min<int64_t>(ppc, a.size[0] - k * ppc);
+        IGG_HIP_CHECK(hipMemcpyAsync(stage_[k], reinterpret_cast<const char*>(a.ptr) + k * ppc * plane,
+                                     static_cast<size_t>(nx) * plane, hipMemcpyDeviceToDevice, stream));
+        rec += ipc_get_handle(stage_[k]);
+      }
+    } else {
+      const uint64_t off = a.ptr - reinterpret_cast<uintptr_t>(base);
+      rec.push_back('D');
+      rec += ipc_get_handle(base);
+      rec.append(reinterpret_cast<const char*>(&off), sizeof(off));
+    }
+  }
+  // `a` (or its staged copy; on the root also dst) is final where the
+  // caller's stream has got to now: an interprocess event marks that point
+  // (no host drain).
+  IGG_HIP_CHECK(hipEventRecord(ready_, stream));
+  hipIpcEventHandle_t eh;
+  IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, ready_));
+  std::string mine(reinterpret_cast<const char*>(&eh), EH);
+  mine += rec;
+  if (rank_ == root) {
     for (hipEvent_t e : done_) {  // the peers order their streams after these in wait()
       IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, e));
       mine.append(reinterpret_cast<const char*>(&eh), EH);
@@ -164,7 +228,7 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
         src = reinterpret_cast<const void*>(a.ptr);
       } else {
         const std::string& rec = all[p];
-        if (rec.size() != EH + MH + 8) fail("gather_async: malformed handles from rank ", p);
+        if (rec.size() < EH + 1) fail("gather_async: malformed handles from rank ", p);
         const std::string ekey = rec.substr(0, EH);
         if (peer_key_[p] != ekey) {  // opened once per peer event
           if (peer_ev_[p]) IGG_HIP_CHECK(hipEventDestroy(peer_ev_[p]));
@@ -174,20 +238,40 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
           peer_key_[p] = ekey;
         }
         IGG_HIP_CHECK(hipStreamWaitEvent(s, peer_ev_[p], 0));
-        uint64_t off = 0;
-        std::memcpy(&off, rec.data() + EH + MH, 8);
-        const std::string mkey = rec.substr(EH, MH);
-        auto& m = mapped_[p];
-        if (m.first != mkey) {  // this rank's array lives in another allocation now
-          if (m.second) {
+        const char mode = rec[EH];
+        const size_t nbuf = mode == 'C' && rec.size() >= EH + 9 ? get_u32(rec, EH + 1) : 1;
+        const size_t hdr = mode == 'C' ? EH + 9 : EH + 1;
+        if ((mode != 'C' && mode != 'D') || (mode == 'D' && rec.size() != hdr + MH + 8) ||
+            (mode == 'C' && rec.size() != hdr + nbuf * MH))
+          fail("gather_async: malformed handles from rank ", p);
+        auto& per = mapped_[p];
+        bool changed = per.size() != nbuf;
+        for (size_t k = 0; k < nbuf && !changed; ++k) changed = per[k].first != rec.substr(hdr + k * MH, MH);
+        if (changed) {  // this rank's array (or staging) lives in other allocations now
+          if (!per.empty()) {
             for (hipStream_t q : side_) IGG_HIP_CHECK(hipStreamSynchronize(q));  // rare: old copies drained
-            ipc_close(m.second);
+            for (auto& m : per) ipc_close(m.second);
           }
-          m = {mkey, ipc_open(mkey)};
+          per.clear();
+          for (size_t k = 0; k < nbuf; ++k) {
+            const std::string key = rec.substr(hdr + k * MH, MH);
+            per.emplace_back(key, ipc_open(key));
+          }
         }
-        src = static_cast<const char*>(m.second) + off;
+        if (mode == 'C') {
+          const int64_t ppc = get_u32(rec, EH + 5);
+          for (size_t k = 0; k < nbuf; ++k) {
+            const int64_t x0 = static_cast<int64_t>(k) * ppc;
+            copy_block(per[k].second, dst, a.size, dims, c, x0, std::min<int64_t>(ppc, a.size[0] - x0),
+                       a.elem_bytes, s);
+          }
+          continue;
+        }
+        uint64_t off = 0;
+        std::memcpy(&off, rec.data() + hdr + MH, 8);
+        src = static_cast<const char*>(per[0].second) + off;
       }
-      copy_block(src, dst, a.size, dims, c, a.elem_bytes, s);
+      copy_block(src, dst, a.size, dims, c, 0, a.size[0], a.elem_bytes, s);
     }
     for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipEventRecord(done_[k], side_[k]));
   } else {

@@ -64,6 +64,14 @@ class Gatherer {
 // `a` is read-only until then) queues behind the pulls on the device.
 // Peer mappings are cached per rank and closed when that rank's allocation
 // changes (after the copy streams drained) or at free().
+// Large blocks: an IPC handle of an allocation of 2 GiB or more cannot be
+// opened on this runtime (ipc.hpp IPC_MAX_BYTES). A rank whose allocation
+// holding `a` is that large (or, for tests, larger than IGG_GATHER_CHUNK_BYTES)
+// first copies `a` on its stream into grow-only staging chunks of whole
+// x-planes, each its own exportable allocation (< 1 GiB by default), and
+// publishes the chunks' handles; the root pulls each chunk as a 3-D sub-block.
+// The staging copy precedes the ready event, and the next gather's copy
+// follows wait()'s ordering behind the root's pulls, like `a` itself.
 class PullGatherer {
  public:
   using AllGather = std::function<std::vector<std::string>(const std::string&)>;
@@ -89,7 +97,11 @@ class PullGatherer {
   std::vector<hipEvent_t> peer_ev_;    // opened peer events (root)
   std::vector<std::string> root_key_;  // non-root: the root's done-event handles (cache keys)
   std::vector<hipEvent_t> root_done_;  // non-root: the root's done events, opened
-  std::vector<std::pair<std::string, void*>> mapped_;  // root: per rank (handle, base) of `a`'s allocation
+  // root: per rank, per published buffer (one: `a`'s allocation; or its
+  // staging chunks) the (handle, mapped base)
+  std::vector<std::vector<std::pair<std::string, void*>>> mapped_;
+  std::vector<char*> stage_;  // own staging chunks (a large `a`), grow-only
+  size_t stage_bytes_ = 0;    // bytes of each staging chunk
   bool pending_ = false;
   int root_ = 0;
   int used_ = 0;  // copy streams used by the pending gather

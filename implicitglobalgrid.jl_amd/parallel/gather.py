@@ -8,8 +8,8 @@ gathered into a 3-D ``A_global``); ``A_global`` may be ``None`` off-root; the
 root keeps a grow-only internal buffer until ``finalize_global_grid``.
 
 MI355X paths (csrc/gather.cpp):
-* GPU ``A``, all ranks on one node, allocations below the IPC size limit
-  (the default; IGG_GATHER_PULL=0 disables):
+* GPU ``A``, all ranks on one node (the default; IGG_GATHER_PULL=0 disables;
+  a block in an allocation too large to export is staged in chunks first):
   the root's copy engines pull every block over xGMI straight into its place
   in ``A_global`` (one 3-D peer copy per block, up to 8 concurrent copy
   streams, ordered by interprocess events): no staging buffer of
@@ -52,17 +52,13 @@ def free_gather_buffer() -> None:
 
 
 def _pull_ok(gg, A: torch.Tensor) -> bool:
-    """Pull path for GPU fields: every rank on this node (IPC-mappable peers)
-    and every rank's allocation holding ``A`` below the IPC size limit
-    (``native.IPC_MAX_BYTES``: opening a larger handle hangs on this ROCm
-    runtime, csrc/include/igg/ipc.hpp). Collective (one gloo all-reduce); the
-    same answer on every rank."""
+    """Pull path for GPU fields: every rank on this node (IPC-mappable peers).
+    The same answer on every rank (the choice is collective). A rank whose
+    allocation holding ``A`` is too large to export (``native.IPC_MAX_BYTES``:
+    opening a larger handle hangs on this ROCm runtime) stages ``A`` into
+    exportable chunks itself (csrc/include/igg/gather.hpp PullGatherer)."""
     c = gg.comm
-    if not (int(gg.nprocs) > 1 and c is not None and c.local_size == c.size and config.gather_pull()):
-        return False
-    t = torch.tensor([float(native.alloc_bytes(A.data_ptr()))], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=c.gloo)
-    return float(t.item()) < float(native.IPC_MAX_BYTES)
+    return int(gg.nprocs) > 1 and c is not None and c.local_size == c.size and config.gather_pull()
 
 
 def _padded_shape(A: torch.Tensor) -> list[int]:
@@ -201,8 +197,8 @@ def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int =
     gg = _grid.global_grid()
     nprocs, me = int(gg.nprocs), int(gg.me)
     if not (A.is_cuda and nprocs > 1) or not _pull_ok(gg, A):
-        # one process, or not IPC-mappable (another node, or an allocation
-        # above the IPC size limit): the synchronous gather_ (RCCL / host)
+        # one process, or not IPC-mappable (another node): the synchronous
+        # gather_ (RCCL / host)
         gather_(A, A_global, root=root)
         return GatherHandle(A_global, True)
     if me == root:

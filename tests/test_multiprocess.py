@@ -115,6 +115,16 @@ def test_gather_async_gpu(nprocs):
     run_ranks(nprocs, "gather_async", env_extra=PUT_ENV)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs", [2, 4])
+def test_gather_pull_staged_chunks_gpu(nprocs):
+    """Blocks too large to export whole (above 2 GiB on the real runtime,
+    above 100 / 400 bytes here) are staged in chunks of whole x-planes and
+    pulled chunk by chunk: gather_async_ (ordering, reuse) and gather_."""
+    run_ranks(nprocs, "gather_async", env_extra=dict(PUT_ENV, IGG_GATHER_CHUNK_BYTES="400"))
+    run_ranks(nprocs, "gather", "gpu", "f64", env_extra=dict(PUT_ENV, IGG_GATHER_CHUNK_BYTES="100"))
+
+
 # --- fused halo exchange (stencil kernel stores into the neighbours' arenas)
 @pytest.mark.gpu
 @pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 0, 0), ("0", "0")),
