@@ -436,11 +436,20 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
     # rows, z-planes of a C-ordered field are maximally strided. (RCCL's p2p
     # kernels next to a full-GPU stencil measured slower than serial in
     # loopback, profiles/r1_ctas/; over real xGMI the A/B decides.)
-    if getattr(model, "can_overlap", False) and not any(model.sides[2]):
+    # Not by default: replaying the captured overlapped put step crashed
+    # (SIGSEGV inside hipGraph replay, every rank) with x AND y neighbours
+    # (4 ranks, 2x2x1, 512^3; 2x1x1 replays fine): profiles/r3_overlap_crash/.
+    # A crash cannot be caught, and the fused exchange is the hiding mechanism
+    # the A/B keeps anyway; IGG_BENCH_OVERLAP=1 puts them back.
+    if (os.environ.get("IGG_BENCH_OVERLAP") == "1" and getattr(model, "can_overlap", False)
+            and not any(model.sides[2])):
         if valid.get("put") == "ok":
             cands.append(("put+overlap", "put", "auto", True))
         if valid.get("rccl-sequential") == "ok":
             cands.append(("rccl+overlap", "rccl", "sequential", True))
+    only = os.environ.get("IGG_BENCH_SCHEDULES")  # diagnosis: "put,put+overlap,..." limits the A/B
+    if only:
+        cands = [c for c in cands if c[0] in only.split(",")]
     if not cands:
         raise RuntimeError("no device transport passed the bitwise validation against the host-staged path")
     times = {}
@@ -628,9 +637,10 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
 
 def main():
     args = parse()
-    if os.environ.get("IGG_BENCH_STACKS"):  # diagnosis of a hang: every rank's Python stack every N s
-        import faulthandler
+    import faulthandler
 
+    faulthandler.enable()  # a fatal signal (segfault, abort) prints the rank's Python stack
+    if os.environ.get("IGG_BENCH_STACKS"):  # diagnosis of a hang: every rank's Python stack every N s
         faulthandler.dump_traceback_later(float(os.environ["IGG_BENCH_STACKS"]), repeat=True)
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:

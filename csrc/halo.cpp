@@ -433,13 +433,23 @@ void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stre
   if (!g.has_peers) fail("the put transport needs the peer table (GridInfo.peers)");
   const size_t nf = fields.size();
   const int eb = fields[0].elem_bytes;
-  // Arena slot of (key, field): a function of the field shapes only, so every
-  // rank computes the same layout for the same call.
+  // Arena slot of (key, field): a function of the field shapes and of the
+  // dimensions in which the grid has neighbours at all, so every rank computes
+  // the same layout for the same call. (A dimension has neighbours on every
+  // rank or on none: periodic, or split over >= 2 ranks, gives each rank at
+  // least one.) Directions along a dimension without neighbours get no slot:
+  // for a 2-D field (nz = 1) a "z face" would be the whole field, and 2 x 26
+  // such slots made the acoustic model's arena exceed the IPC size limit.
+  bool dim_has_nb[NDIMS];
+  for (int d = 0; d < NDIMS; ++d) dim_has_nb[d] = g.neighbors[0][d] != PROC_NULL || g.neighbors[1][d] != PROC_NULL;
   std::vector<size_t> slot(27 * nf, 0);
+  bool has_slot[27] = {};
   size_t per = 0;
   for (int key = 0; key < 27; ++key) {
     if (key == 13) continue;
     const int u[3] = {key / 9 - 1, (key / 3) % 3 - 1, key % 3 - 1};
+    if ((u[0] != 0 && !dim_has_nb[0]) || (u[1] != 0 && !dim_has_nb[1]) || (u[2] != 0 && !dim_has_nb[2])) continue;
+    has_slot[key] = true;
     for (size_t i = 0; i < nf; ++i) {
       int64_t elems = 1;
       for (int d = 0; d < NDIMS; ++d) elems *= u[d] != 0 ? 1 : fields[i].size[d];
@@ -460,6 +470,10 @@ void HaloEngine::exchange_put(const std::vector<Field>& fields, hipStream_t stre
   for (int key = 0; key < 27; ++key) {
     if (key == 13) continue;
     const int64_t from = g.peers[key], to = g.peers[26 - key];
+    if (!has_slot[key]) {
+      if (from != PROC_NULL || to != PROC_NULL) fail("put transport: a peer along a dimension without neighbours");
+      continue;
+    }
     if (from != PROC_NULL) add(nb_ranks, static_cast<int>(from));
     for (size_t i = 0; i < nf; ++i) {
       const Field& f = fields[i];
