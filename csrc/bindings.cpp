@@ -569,6 +569,8 @@ PYBIND11_MODULE(_igg_native, m) {
       .def("drain", [](FusedAcoustic& f, uintptr_t s) { f.drain(as_stream(s)); }, py::arg("stream"),
            "Exit barrier after in-kernel synchronised steps (collective; no-op after a sync-kernel step).")
       .def("check_error", &FusedAcoustic::check_error)
+      .def("clear_error", &FusedAcoustic::clear_error,
+           "Reset this rank's sticky timeout word (after a failed exchange was handled).")
       .def("set_step_sync", &FusedAcoustic::set_step_sync, py::arg("mode"),
            "Step synchronisation: -1 default, 0 inside the fused kernel, 1 sync kernel (same on every rank).")
       .def_property_readonly("in_kernel_sync", &FusedAcoustic::in_kernel_sync)
@@ -657,6 +659,8 @@ PYBIND11_MODULE(_igg_native, m) {
       .def_property_readonly("zpitch", &FusedHalo::zpitch)
       .def_property_readonly("n_peers", &FusedHalo::n_peers)
       .def("check_error", [](FusedHalo& f) { f.mesh().check_error(); })
+      .def("clear_error", [](FusedHalo& f) { f.mesh().clear_error(); },
+           "Reset this rank's sticky timeout word (after a failed exchange was handled).")
       .def("set_step_sync", &FusedHalo::set_step_sync, py::arg("mode"),
            "Step synchronisation: -1 default, 0 inside the fused kernel, 1 sync kernel (same on every rank).")
       .def_property_readonly("in_kernel_sync", &FusedHalo::in_kernel_sync)

@@ -92,6 +92,8 @@ void FusedAcoustic::drain(hipStream_t stream) {
 
 void FusedAcoustic::check_error() const { mesh_->check_error(); }
 
+void FusedAcoustic::clear_error() { mesh_->clear_error(); }
+
 uint64_t FusedAcoustic::flag(int index) const { return mesh_->read_flag(index); }
 
 bool FusedAcoustic::in_kernel_sync() const {

@@ -90,6 +90,7 @@ class FusedAcoustic {
   // collective, a sync kernel only if the last step left remote stores open.
   void drain(hipStream_t stream);
   void check_error() const;
+  void clear_error();
   uint64_t flag(int index) const;  // own flag word (PutFlags), host read
   // Step synchronisation form (FusedHalo::set_step_sync).
   void set_step_sync(int mode) { sync_mode_ = mode; }

@@ -142,6 +142,12 @@ class Acoustic2D:
         """No-op: the fused step leaves every halo value as update_halo_ would
         (the API matches Diffusion3D's, whose fused step defers halo planes)."""
 
+    def clear_error(self) -> None:
+        """Reset the fused exchange's sticky timeout word on this rank (after
+        a failed fused step was handled, e.g. the fused exchange was dropped)."""
+        if self._fa is not None:
+            self._fa.clear_error()
+
     def check(self) -> None:
         """Raise if a fused-exchange sync kernel timed out waiting for a neighbour."""
         if self._fa is not None:

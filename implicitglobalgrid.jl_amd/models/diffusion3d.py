@@ -266,6 +266,12 @@ class Diffusion3D:
         self._fentry = True
         return int(meta["step"])
 
+    def clear_error(self) -> None:
+        """Reset the fused exchange's sticky timeout word on this rank (after
+        a failed fused step was handled, e.g. the fused exchange was dropped)."""
+        if self._fh is not None:
+            self._fh.clear_error()
+
     def check(self) -> None:
         """Raise if a fused-exchange sync kernel timed out waiting for a neighbour."""
         if self._fh is not None:
