@@ -132,84 +132,73 @@ def parse():
     return ap.parse_args()
 
 
+def _supervise():
+    """utils/supervise.py, loaded by path: a supervisor never imports the
+    package (nor touches the GPU)."""
+    import importlib.util as ilu
+
+    mod = sys.modules.get("igg_supervise")
+    if mod is None:
+        p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "implicitglobalgrid.jl_amd", "utils",
+                         "supervise.py")
+        spec = ilu.spec_from_file_location("igg_supervise", p)
+        mod = ilu.module_from_spec(spec)
+        sys.modules["igg_supervise"] = mod
+        spec.loader.exec_module(mod)
+    return mod
+
+
+def _share_gpu_env(args, env: dict) -> None:
+    if args.share_gpu and args.gpus > 2:
+        # Rehearsal with every rank on one GPU: N processes x 4 hardware
+        # queues oversubscribe the device's queue slots and the command
+        # processor time-slices them (8 ranks: 7.9 ms/step vs 0.25 with one
+        # queue per process, profiles/r2_reh8/). One rank per GPU never does.
+        # Overrides the environment's value (the GPU boxes export 4).
+        env["GPU_MAX_HW_QUEUES"] = "1"
+
+
 def self_launch(args) -> int:
     """``--gpus N`` without a launcher: start N ranks of this script (one per
     GPU, LOCAL_RANK = GPU index) from this parent, which never touches the GPU
-    (it does not even import torch). Fail-fast: the first rank that exits
-    non-zero stops the others. Prints rank 0's JSON line; non-zero exit if any
-    rank failed, the run timed out, or the line's n_gpus differs from N."""
-    import socket
-    import subprocess
-    import tempfile
-
-    n = args.gpus
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    procs, outs = [], []
-    for r in range(n):
-        env = dict(os.environ)
-        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), IGG_BENCH_SELF_LAUNCHED="1")
-        if args.share_gpu and n > 2:
-            # Rehearsal with every rank on one GPU: N processes x 4 hardware
-            # queues oversubscribe the device's queue slots and the command
-            # processor time-slices them (8 ranks: 7.9 ms/step vs 0.25 with one
-            # queue per process, profiles/r2_reh8/). One rank per GPU never does.
-            # Overrides the environment's value (the GPU boxes export 4).
-            env["GPU_MAX_HW_QUEUES"] = "1"
-        out = tempfile.TemporaryFile(mode="w+")
-        outs.append(out)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
-                                      env=env, stdout=out, stderr=None))
-    deadline = time.monotonic() + args.launch_timeout
-    rc, why = 0, ""
-    try:
-        while True:
-            codes = [p.poll() for p in procs]
-            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
-            if bad:
-                rc, why = 1, f"rank {bad[0][0]} exited with {bad[0][1]}"
-                break
-            if all(c == 0 for c in codes):
-                break
-            if time.monotonic() > deadline:
-                rc, why = 1, f"timed out after {args.launch_timeout:.0f} s"
-                break
-            time.sleep(0.05)
-    except KeyboardInterrupt:
-        rc, why = 130, "interrupted"
-    for p in procs:  # exact child processes of this parent, never by pattern
-        if p.poll() is None:
-            p.terminate()
-    for p in procs:
-        try:
-            p.wait(timeout=15)
-        except subprocess.TimeoutExpired:
-            p.kill()
-            p.wait()
-    outs[0].seek(0)
-    lines = outs[0].read().splitlines()
-    for o in outs:
-        o.close()
-    rec = None
-    for ln in lines:
-        if ln.startswith("{") and '"metric"' in ln:
-            rec = ln
-        else:
-            print(ln, file=sys.stderr)
+    (it does not even import torch), and supervise them
+    (igg/utils/supervise.py): a rank that dies or stalls past its phase
+    deadline stops the attempt, and fresh ranks are started without the path
+    that phase exercised (``config.excluded`` lists it). Prints rank 0's JSON
+    line; non-zero exit if no attempt succeeded, the run timed out, or the
+    line's n_gpus differs from N."""
+    sup = _supervise()
+    argv = [sys.executable, os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, IGG_BENCH_SELF_LAUNCHED="1")
+    rc, rec, excl = sup.run_local(argv, args.gpus, env, timeout=args.launch_timeout,
+                                  env_for_rank=lambda r, e: _share_gpu_env(args, e))
     if rc != 0:
-        print(f"bench self-launch: {why}", file=sys.stderr)
+        print("bench self-launch: no attempt produced a result", file=sys.stderr)
         return rc
     if rec is None:
         print("bench self-launch: rank 0 printed no result line", file=sys.stderr)
         return 1
     got = json.loads(rec).get("n_gpus")
-    if got != n:
-        print(f"bench self-launch: result reports n_gpus={got}, expected {n}", file=sys.stderr)
+    if got != args.gpus:
+        print(f"bench self-launch: result reports n_gpus={got}, expected {args.gpus}", file=sys.stderr)
         return 1
     print(rec, flush=True)
     return 0
+
+
+def launcher_supervise(args) -> int:
+    """Under a launcher (torchrun: WORLD_SIZE set, N > 1) this process becomes
+    the supervisor of its rank: it starts the real worker (same rank / world,
+    a per-attempt rendezvous port) and agrees with the other ranks'
+    supervisors over the launcher's TCP store on done / relaunch without a
+    path / fail (igg/utils/supervise.py). It never touches the GPU."""
+    sup = _supervise()
+    argv = [sys.executable, os.path.abspath(__file__), *sys.argv[1:]]
+    return sup.run_torchrun(argv, timeout=args.launch_timeout, env_adjust=lambda e: _share_gpu_env(args, e))
+
+
+def _first_contact() -> float:
+    return float(os.environ.get("IGG_FIRST_CONTACT_TIMEOUT", "120"))
 
 
 def _max_over_ranks(comm, v: float) -> float:
@@ -291,6 +280,50 @@ def _step_estimate_ms(model, comm) -> float:
     return max(0.05, _max_over_ranks(comm, (time.perf_counter() - t0) * 1e3 / k))
 
 
+class _NoPhases:
+    def enter(self, *a, **k):
+        pass
+
+    def printed(self):
+        pass
+
+    def relaunch(self, keys, code=3):
+        raise SystemExit(f"bench: relaunch without {sorted(keys)} requested outside a supervisor")
+
+
+# Phase announcements to the supervisor and the paths excluded by it (set in
+# main; igg/utils/supervise.py). Exclusion keys: rccl, put, fused,
+# fused-inkernel, graph, host-ordered, host-tagged.
+PH = _NoPhases()
+EXCL: dict = {}
+
+
+def _transport_key(t: str) -> str | None:
+    return {"rccl": "rccl", "put": "put", "torch": "rccl"}.get(t)
+
+
+def _path_key(model) -> str | None:
+    """Exclusion key of what a time step of the model currently exercises."""
+    from igg.parallel import halo as H
+
+    if getattr(model, "fused", False):
+        return "fused-inkernel" if getattr(model, "fused_mode", 0) & 16 else "fused"
+    return _transport_key(H.transport_name())
+
+
+def _check_abandoned(comm, key: str, what: str, log) -> None:
+    """A bounded first-contact call (RCCL bootstrap, IPC open) that had to be
+    abandoned leaves a thread stuck in the HIP runtime: such a process is not
+    trusted with more GPU work. If it happened on any rank, every rank asks
+    the supervisor for fresh processes without ``key`` (collective)."""
+    from igg import native
+
+    n = native.abandoned_waits() + (1 if _inject(f"abandon-{key}") else 0)  # test hook
+    if _max_over_ranks(comm, float(n)) > 0:
+        log(f"bench: {what}: a bounded first-contact call was abandoned; relaunching without {key!r}")
+        PH.relaunch({key: f"{what}: a first-contact call (RCCL bootstrap / IPC open) was abandoned"})
+
+
 def _probe_field(field):
     """Rank-distinct payload (exact in fp64) with every boundary plane poisoned,
     so a missing, misplaced or wrong-rank receive cannot go unnoticed."""
@@ -332,6 +365,13 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
     for name, t, mode in TRANSPORT_CANDIDATES:
         if names is not None and name not in names:
             continue
+        key = _transport_key(t)
+        if key in EXCL:
+            out[name] = f"excluded: {EXCL[key]}"
+            log(f"validation {name}: {out[name]}")
+            continue
+        # deadline: a bounded first contact (IGG_FIRST_CONTACT_TIMEOUT) + the exchange
+        PH.enter(f"validate:{name}", key, deadline=2 * _first_contact() + 120)
         why = ""
         try:
             H.set_transport(t)  # collective: creates the RCCL communicator / put mesh on first use
@@ -351,6 +391,7 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
         fails = _max_over_ranks(comm, 1.0 if why else 0.0)
         out[name] = "ok" if fails == 0.0 else (why or "failed on another rank")
         log(f"validation {name} vs {ref}: {out[name]}")
+        _check_abandoned(comm, key, f"validation of {name}", log)
     H.set_transport("rccl" if out.get("rccl-sequential") == "ok" else ref)
     H.set_halo_mode("auto")
     del X0, R
@@ -362,7 +403,8 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
     the transport and schedule the timed steps used, compared bitwise with the
     host-staged gloo exchange (the reference's non-GPU-aware path). Collective;
     every rank agrees. The transport / schedule settings are restored.
-    (CPU plumbing runs have one path only: the comparison is with itself.)"""
+    (CPU plumbing runs: the timed host matching form against the other one,
+    order-only vs tagged, unless that one is excluded.)"""
     import torch
 
     from igg.parallel import halo as H
@@ -372,7 +414,9 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
         t, gmode = H.transport_name(), H.halo_mode()
         sched = "put" if t == "put" else H.plan_mode(field)
     else:
-        t, gmode, sched = "host", None, "sequential"
+        m = os.environ.get("IGG_HOST_MATCHING", "ordered")
+        t, gmode, sched = f"host-{m}", None, "sequential"
+        other = "tagged" if m == "ordered" else "ordered"
     why = ""
     if os.environ.get("IGG_BENCH_DEBUG_POST") and on_gpu and t == "put":  # diagnostics (collective)
         eps = comm.all_gather_object(int(comm.mesh.epoch))
@@ -388,6 +432,8 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
         if on_gpu:
             H.set_transport("staged")
             H.set_halo_mode("sequential")
+        elif f"host-{other}" not in EXCL:
+            os.environ["IGG_HOST_MATCHING"] = other
         R = X0.clone()
         H.update_halo_(R)
         if on_gpu:
@@ -419,9 +465,11 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
         if on_gpu:
             H.set_transport(t)
             H.set_halo_mode(gmode)
+        else:
+            os.environ["IGG_HOST_MATCHING"] = m
     fails = _max_over_ranks(comm, 1.0 if why else 0.0)
     res = "ok" if fails == 0.0 else (why or "failed on another rank")
-    log(f"post-timing validation {t}/{sched} vs staged: {res}")
+    log(f"post-timing validation {t}/{sched} vs {'staged' if on_gpu else 'host-' + other}: {res}")
     return {"transport": t, "schedule": sched, "result": res}
 
 
@@ -454,6 +502,7 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
         raise RuntimeError("no device transport passed the bitwise validation against the host-staged path")
     times = {}
     for name, t, mode, ov in cands:
+        PH.enter(f"ab:{name}", _transport_key(t), deadline=300)
         H.set_transport(t)
         H.set_halo_mode(mode)
         if hasattr(model, "set_overlap"):
@@ -580,7 +629,14 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
     passes). ``mode``: auto (keep the faster), on (force when it checks out), off."""
     if mode == "off" or not getattr(model, "can_fuse", False):
         return None
-    if not _fused_check(model, comm, log):
+    if "fused" in EXCL:
+        log(f"fused halo exchange: excluded ({EXCL['fused']})")
+        return {"fused_ok": False, "excluded": EXCL["fused"]}
+    # the first switch-on maps the neighbours' arenas and fields (IPC, bounded)
+    PH.enter("fused:check", "fused", deadline=2 * _first_contact() + 300)
+    ok = _fused_check(model, comm, log)
+    _check_abandoned(comm, "fused", "fused exchange setup", log)
+    if not ok:
         log("fused halo exchange mismatched the update_halo_ path on some rank: excluded")
         return {"fused_ok": False}
     diffusion = hasattr(model, "fused_variant")
@@ -608,15 +664,35 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
             model.fused_variant, model.fused_mode, model.fused_rounds = c
 
     name = (lambda k: f"v{k[0]}/m{k[1]}/r{k[2]}") if diffusion else (lambda k: "fused")  # noqa: E731
+    ckey = (lambda k: "fused-inkernel" if k is not None and k[1] & 16 else "fused")  # noqa: E731
+    unf_key = _path_key(model)
     t_unf, times = float("inf"), {}
-    for _ in range(2):
-        model.set_fused(False)
-        t_unf = min(t_unf, _timed_candidate(model, comm, 20, graph))
-        model.set_fused(True)
-        for c in cands:
-            use(c)
-            t = _timed_candidate(model, comm, 20, graph)
-            times[c] = min(times.get(c, float("inf")), t)
+
+    def timing_passes(cs):
+        nonlocal t_unf
+        for _ in range(2):
+            PH.enter("fused:ab:update_halo", unf_key, deadline=300)
+            model.set_fused(False)
+            t_unf = min(t_unf, _timed_candidate(model, comm, 20, graph))
+            model.set_fused(True)
+            for c in cs:
+                use(c)
+                PH.enter(f"fused:ab:{name(c)}", ckey(c), deadline=300)
+                t = _timed_candidate(model, comm, 20, graph)
+                times[c] = min(times.get(c, float("inf")), t)
+
+    timing_passes(cands)
+    # The step synchronisation inside the fused kernel (send mode bit 16, put.hpp
+    # StepSync) is a candidate of its own: the two fastest sync-kernel forms are
+    # re-timed with it, where it is allowed (not where ranks share a GPU, not
+    # excluded by the supervisor after a failure). Its kept check below is the
+    # same 200-step bitwise check; if it fails, the next fastest form - a
+    # sync-kernel one - is kept.
+    if (diffusion and "fused-inkernel" not in EXCL and model._fh is not None
+            and model._fh.in_kernel_sync_for(16) and not model._fh.in_kernel_sync_for(0)
+            and os.environ.get("IGG_FUSED_INKERNEL", "1") != "0"):
+        front = [c for c, _t in sorted(times.items(), key=lambda kv: kv[1]) if not c[1] & 16][:2]
+        timing_passes([(v, fm | 16, gr) for v, fm, gr in front])
     model.set_fused(False)
     model.graph = None
     keep, best, rejected = False, None, []
@@ -625,6 +701,7 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
             break
         use(cand)
         # the kept candidate: a long check whatever the quick one said
+        PH.enter(f"fused:keep:{name(cand)}", ckey(cand), deadline=600)
         if _fused_check(model, comm, log, nchk=FUSED_KEEP_CHECK_STEPS):
             keep, best = True, cand
             break
@@ -645,6 +722,118 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
     return out
 
 
+def _second_variant(model):
+    """A compiled stencil variant other than the timed one (every rank picks
+    the same: the autotune's ranking is summed over ranks), or None on CPU."""
+    if getattr(model, "variant", None) is None:
+        return None
+    from igg.ops import stencil
+
+    ranked = []
+    for k, t in sorted((model.variant_times or {}).items(), key=lambda kv: kv[1]):
+        v = int(k.split("@")[0])
+        if v not in ranked:
+            ranked.append(v)
+    compiled = set(stencil.compiled_variants())
+    for v in ranked + list(stencil.SHORTLIST):
+        if v != model.variant and v in compiled:
+            return v
+    return None
+
+
+def stencil_post_check(model, comm, log, pre: dict, k: int, on_gpu: bool) -> dict:
+    """After the timed region (update_halo_ path, any N): restore the state
+    the timed steps started from, run the same ``k`` steps eagerly with a
+    SECOND compiled stencil variant (bitwise interchangeable by construction,
+    tests/test_gpu_stencil.py) and compare the result bitwise with the field
+    the timed steps produced. A mismatch means the timed run computed a wrong
+    field: the caller prints no number. Collective (every rank agrees).
+    Leaves the model in the timed end state. (CPU plumbing: the host kernel
+    again, i.e. a determinism check.)"""
+    import torch
+
+    names = _state(model)
+    done = {n: getattr(model, n).clone() for n in names}
+    v_timed, graph = getattr(model, "variant", None), model.graph
+    v2 = _second_variant(model) if on_gpu else None
+    why = ""
+    try:
+        for n in names:
+            getattr(model, n).copy_(pre[n])
+        if hasattr(model, "mark_modified"):
+            model.mark_modified()
+        model.graph = None
+        if v2 is not None:
+            model.variant = v2
+        model.run(k)
+        if on_gpu:
+            _sync(comm)
+        if _inject("stencil_post"):
+            t = getattr(model, names[0])
+            t.view(-1)[t.numel() // 2] += 1
+        cmp = _compared(model)
+        bad = [n for n in cmp if not torch.equal(getattr(model, n), done[n])]
+        if bad:
+            d = (getattr(model, bad[0]) != done[bad[0]]).nonzero()
+            why = f"{bad[0]} differs in {d.shape[0]} entries, first {d[0].tolist()}"
+    except Exception as e:
+        why = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        model.variant = v_timed
+        for n in names:
+            getattr(model, n).copy_(done[n])
+        if hasattr(model, "mark_modified"):
+            model.mark_modified()
+        model.graph = graph
+    fails = _max_over_ranks(comm, 1.0 if why else 0.0)
+    res = "ok" if fails == 0.0 else (why or "failed on another rank")
+    log(f"post-timing stencil check ({k} steps, variant {v_timed} vs {v2 if v2 is not None else 'same'}): {res}")
+    return {"steps": k, "variant": v_timed, "check_variant": v2, "result": res}
+
+
+def validate_host_matching(field, comm, log) -> dict:
+    """CPU plumbing runs with several ranks: the probe payload through the
+    order-only host matching (one tag-0 message per peer and phase, paired by
+    issue order - RCCL's rule) and through the tagged one; both must agree
+    bitwise. Excluded forms are skipped; the first that passes is used."""
+    import torch
+
+    from igg.parallel import halo as H
+
+    X0 = _probe_field(field)
+    outs, res = {}, {}
+    for name in ("host-ordered", "host-tagged"):
+        if name in EXCL:
+            res[name] = f"excluded: {EXCL[name]}"
+            continue
+        PH.enter(f"validate:{name}", name, deadline=300)
+        os.environ["IGG_HOST_MATCHING"] = name.split("-")[1]
+        X = X0.clone()
+        try:
+            H.update_halo_(X)
+            outs[name] = X
+        except Exception as e:
+            res[name] = f"{type(e).__name__}: {e}"[:300]
+        _check_abandoned(comm, name, f"validation of {name}", log)
+    if len(outs) == 2:
+        same = torch.equal(outs["host-ordered"], outs["host-tagged"])
+        if _inject("host_matching") or not same:
+            res["host-ordered"] = res["host-tagged"] = "the two matching forms disagree"
+    for name in outs:
+        res.setdefault(name, "ok")
+    for name in ("host-ordered", "host-tagged"):
+        if name in res and name not in EXCL:
+            fails = _max_over_ranks(comm, 0.0 if res[name] == "ok" else 1.0)
+            if fails and res[name] == "ok":
+                res[name] = "failed on another rank"
+    ok = [n for n in ("host-ordered", "host-tagged") if res.get(n) == "ok"]
+    if not ok:
+        raise RuntimeError(f"no host matching form passed the probe exchange: {res}")
+    os.environ["IGG_HOST_MATCHING"] = ok[0].split("-")[1]
+    log(f"host matching validation: {res} -> {ok[0]}")
+    return res
+
+
 def main():
     args = parse()
     import faulthandler
@@ -659,6 +848,13 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report an "
                          f"{world}-process number as an {args.gpus}-GPU one")
+    if (world > 1 and os.environ.get("IGG_SUP_CHILD") != "1"
+            and os.environ.get("IGG_BENCH_SUPERVISE", "1") != "0"):
+        sys.exit(launcher_supervise(args))
+    global PH, EXCL
+    sup = _supervise()
+    PH, EXCL = sup.Phases(), sup.excluded()
+    PH.enter("init", None, deadline=600)
     import torch
 
     import igg
@@ -685,6 +881,8 @@ def main():
     os.environ.setdefault("IGG_PUT_TIMEOUT", "20")
     if args.share_gpu:
         os.environ.setdefault("IGG_TRANSPORT", "staged")
+    if "gather-pull" in EXCL:
+        os.environ["IGG_GATHER_PULL"] = "0"
     me, dims, nprocs, coords, comm = igg.init_global_grid(
         n, n, 1 if is2d else n, periodx=perx, periody=pery, periodz=0 if is2d else perz, quiet=True,
         select_device=on_gpu and not args.share_gpu, device_type="auto" if on_gpu else "none")
@@ -697,6 +895,7 @@ def main():
         lb = (bool(perx), bool(pery), bool(perz)) if pdims else (True, True, True)
         H.enable_loopback((lb[0], lb[1], lb[2] and not is2d))
     dev = None if on_gpu else "cpu"
+    PH.enter("model", None, deadline=900)  # allocation + stencil autotune
     model = Acoustic2D(dtype=dtype) if is2d else Diffusion3D(dtype=dtype, overlap=args.overlap, device=dev)
     field = (lambda: model.P) if is2d else (lambda: model.T)
     sync = (lambda: _sync(comm)) if on_gpu else (lambda: None)
@@ -705,7 +904,7 @@ def main():
         # gather_ concatenates the local blocks (halos included) in Cartesian order
         A_global = torch.empty([int(d) * int(s) for d, s in zip(dims, field().shape)],
                                dtype=dtype, device=field().device)
-    graph_ok = args.graph and on_gpu
+    graph_ok = args.graph and on_gpu and "graph" not in EXCL
     _BRACKET["gpu"], _BRACKET["dev"] = on_gpu, False
     valid, ab = None, None
     if on_gpu and nprocs > 1:
@@ -725,13 +924,18 @@ def main():
             H.set_halo_mode(first[2])
         else:
             raise RuntimeError("no device transport passed the bitwise validation")
+    host_valid = None
+    if not on_gpu and nprocs > 1:
+        host_valid = validate_host_matching(field(), comm, log)
     fused_ab = None
     if on_gpu and not args.overlap and (nprocs > 1 or args.loopback or pdims):
         fused_ab = select_fused(model, comm, log, args.fused, graph_ok)
+    PH.enter("warmup", _path_key(model), deadline=300)
     for _ in range(args.warmup):
         model.step()
     graph_error = None
     if graph_ok:
+        PH.enter("capture", "graph", deadline=300)
         try:
             model.capture()
         except Exception as e:  # capture unsupported here: time eager steps
@@ -747,15 +951,28 @@ def main():
     # timed region. The timed region itself is unchanged: exactly K full steps.
     extra = 0
     warm_ms = float(os.environ.get("IGG_BENCH_WARM_MS", "40"))
+    PH.enter("warmup", _path_key(model), deadline=300)
     if on_gpu and warm_ms > 0:
         est = _step_estimate_ms(model, comm)
         k = max(1, getattr(model, "graph_steps", 1) if getattr(model, "graph", None) is not None else 1)
         extra = int(-(-warm_ms // (est * k))) * k
         model.run(extra)
+    pre = {}  # the state a non-fused timed region starts from (stencil_post_check)
+
     def timed_region() -> float:
         """The timed region: exactly ``args.steps`` full steps (plus the
         configured gathers) between two barrier+synchronize brackets; MAX over
-        ranks of the wall time."""
+        ranks of the wall time. The starting state is saved first (outside the
+        brackets) for the post-timing stencil check."""
+        PH.enter("timed", _path_key(model), deadline=600)
+        if not getattr(model, "fused", False):
+            for nm in _state(model):
+                src = getattr(model, nm)
+                if nm not in pre:
+                    pre[nm] = torch.empty_like(src)
+                pre[nm].copy_(src)
+        else:
+            pre.clear()
         sync()
         _bracket(comm)
         t0 = time.perf_counter()
@@ -799,6 +1016,7 @@ def main():
     #     fails (no JSON line) when none is left.
     fused_post = None
     if getattr(model, "fused", False):
+        PH.enter("post:fused", _path_key(model), deadline=600)
         n_post = max(args.steps, FUSED_KEEP_CHECK_STEPS)
         ok = _fused_check(model, comm, log, nchk=n_post, inject="fused_post")
         fused_post = {"steps": n_post, "result": "ok" if ok else "mismatch"}
@@ -815,6 +1033,7 @@ def main():
             H.check_transport()
     post_valid = None
     if nprocs > 1:
+        PH.enter("post:transport", _path_key(model), deadline=300)
         post_valid = post_validate(field(), comm, log, on_gpu)
         tried = [(post_valid["transport"], post_valid["schedule"])]
         while post_valid["result"] != "ok":
@@ -839,6 +1058,18 @@ def main():
             failed = post_valid
             post_valid = post_validate(field(), comm, log, on_gpu)
             post_valid["replaced"] = failed
+    # 3. every non-fused run (N = 1 included): the same K steps from the saved
+    #    starting state through a second compiled stencil variant, bitwise;
+    #    a mismatch fails closed (no JSON line).
+    stencil_post = None
+    if pre and not getattr(model, "fused", False):
+        PH.enter("post:stencil", _path_key(model), deadline=300)
+        stencil_post = stencil_post_check(model, comm, log, pre, args.steps, on_gpu)
+        if stencil_post["result"] != "ok":
+            log(f"bench: post-timing stencil check failed ({stencil_post['result']}): no result")
+            raise SystemExit(1)
+    pre.clear()
+    PH.enter("report", None, deadline=300)
     t_it = elapsed / args.steps
     per_gpu = model.a_eff_bytes / t_it / 1e9
     total = per_gpu * nprocs
@@ -903,8 +1134,12 @@ def main():
                 "halo_schedule": (H.plan_mode(field()) if H.transport_name() != "put" else "put")
                 if nprocs > 1 or args.loopback else None,
                 "halo_mode_measured": H.tuned_modes() or None,
-                "validation": valid,
+                "validation": valid if on_gpu else host_valid,
                 "post_validation": post_valid,
+                "stencil_post_check": stencil_post,
+                "excluded": EXCL or None,
+                "supervisor_attempt": (int(os.environ["IGG_SUP_ATTEMPT"]) if "IGG_SUP_ATTEMPT" in os.environ
+                                       else None),
                 "fused_post_check": fused_post,
                 "transport_ab_ms": ab,
                 "fused_halo": bool(getattr(model, "fused", False)),
@@ -928,6 +1163,8 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+    PH.printed()
+    PH.enter("finalize", None, deadline=120)
     if hasattr(model, "close"):
         model.close()  # collective: unmap the fused exchange's peer arenas
     igg.finalize_global_grid()

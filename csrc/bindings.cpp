@@ -15,6 +15,7 @@
 #include "igg/acoustic.hpp"
 #include "igg/comm.hpp"
 #include "igg/copy.hpp"
+#include "igg/fault.hpp"
 #include "igg/fused.hpp"
 #include "igg/gather.hpp"
 #include "igg/halo.hpp"
@@ -244,6 +245,13 @@ PYBIND11_MODULE(_igg_native, m) {
     return py::bytes(out);
   });
   m.def("rccl_version", &rccl_version);
+  m.def("abandoned_waits", &abandoned_waits,
+        "Bounded first-contact calls this process gave up on (their helper threads are still stuck in the "
+        "runtime): a process with any should be replaced, not reused (fault.hpp).");
+  m.def("first_contact_timeout", &first_contact_timeout);
+  m.def("install_crash_handler", &install_crash_handler,
+        "Print a native backtrace on SIGSEGV/SIGBUS/SIGABRT, then chain to the previous handler "
+        "(faulthandler's Python stack).");
   m.def("trace_enabled", &trace_enabled);
   m.def("trace_push", [](const std::string& n) { trace_push(n.c_str()); });
   m.def("trace_pop", &trace_pop);
@@ -396,13 +404,15 @@ PYBIND11_MODULE(_igg_native, m) {
         auto v = RcclComm::unique_id();
         return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
       })
-      .def(py::init([](py::bytes uid, int nranks, int rank) {
+      .def(py::init([](py::bytes uid, int nranks, int rank, double timeout) {
              std::string s = uid;
              std::vector<uint8_t> v(s.begin(), s.end());
-             py::gil_scoped_release nogil;  // blocking rendezvous
-             return std::make_shared<RcclComm>(v, nranks, rank);
+             py::gil_scoped_release nogil;  // bounded rendezvous (polled)
+             return std::make_shared<RcclComm>(v, nranks, rank, timeout);
            }),
-           py::arg("uid"), py::arg("nranks"), py::arg("rank"))
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("timeout") = 0.0,
+           "Bounded RCCL bootstrap (non-blocking communicator polled for `timeout` s; <= 0: "
+           "IGG_FIRST_CONTACT_TIMEOUT, default 120); aborts and raises on expiry.")
       .def("barrier", [](RcclComm& c, uintptr_t s) { c.barrier(as_stream(s)); })
       .def("allreduce",
            [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t s) {
@@ -663,7 +673,10 @@ PYBIND11_MODULE(_igg_native, m) {
            "Reset this rank's sticky timeout word (after a failed exchange was handled).")
       .def("set_step_sync", &FusedHalo::set_step_sync, py::arg("mode"),
            "Step synchronisation: -1 default, 0 inside the fused kernel, 1 sync kernel (same on every rank).")
-      .def_property_readonly("in_kernel_sync", &FusedHalo::in_kernel_sync)
+      .def_property_readonly("in_kernel_sync", [](const FusedHalo& f) { return f.in_kernel_sync(0); },
+                             "Whether a step with the default send mode synchronises inside the kernel.")
+      .def("in_kernel_sync_for", &FusedHalo::in_kernel_sync, py::arg("mode"),
+           "Whether a step with send mode `mode` synchronises inside the kernel (bit 16 asks for it).")
       .def("flag", [](FusedHalo& f, int i) { return f.mesh().read_flag(i); }, py::arg("index"),
            "Word `index` of this rank's flag block (PutFlags: 0 EPOCH = completed steps, 2 COUNT).")
       .def("close", [](FusedHalo& f) { f.close(); });

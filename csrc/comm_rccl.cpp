@@ -2,13 +2,16 @@
 // Replaces the reference's per-(side, field) MPI.Irecv!/Isend with tag 0
 // (update_halo.jl:713-735) by one ncclGroupStart/End of raw-byte ncclSend/ncclRecv
 // per exchange phase on the halo stream.
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
 #include "igg/comm.hpp"
+#include "igg/fault.hpp"
 
 #define IGG_NCCL_CHECK(expr)                                                        \
   do {                                                                              \
@@ -30,23 +33,41 @@ std::vector<uint8_t> RcclComm::unique_id() {
   return out;
 }
 
-RcclComm::RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank)
-    : rank_(rank), nranks_(nranks) {
+RcclComm::RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank, double timeout_s)
+    : rank_(rank), nranks_(nranks), timeout_s_(timeout_s > 0 ? timeout_s : first_contact_timeout()) {
   if (uid.size() != sizeof(ncclUniqueId)) fail("RcclComm: bad unique id size ", uid.size());
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  // Non-blocking communicator: the bootstrap (a TCP rendezvous of all ranks,
+  // then the topology exchange) runs in RCCL's background and this thread
+  // polls it with a deadline, so a rank that never arrives fails the
+  // initialisation instead of blocking it forever; ncclCommAbort then
+  // releases the half-built communicator. IGG_RCCL_BLOCKING=1 restores the
+  // blocking form.
+  const char* blk = std::getenv("IGG_RCCL_BLOCKING");
+  cfg.blocking = (blk && blk[0] == '1') ? 1 : 0;
   // IGG_RCCL_MAX_CTAS caps the workgroups (channels) of RCCL's kernels, which
   // otherwise take CUs from a concurrently running interior stencil in the
   // overlapped step (RCCL interplay). Unset = RCCL's default.
   const char* env = std::getenv("IGG_RCCL_MAX_CTAS");
   const int max_ctas = env ? std::atoi(env) : 0;
   if (max_ctas > 0) {
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.minCTAs = 1;
     cfg.maxCTAs = max_ctas;
-    IGG_NCCL_CHECK(ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg));
-  } else {
-    IGG_NCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+  }
+  inject_delay("rccl_init");
+  const ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (comm_) (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+    fail("RCCL error '", ncclGetErrorString(r), "' in ncclCommInitRankConfig (rank ", rank, " of ", nranks, ")");
+  }
+  try {
+    wait_ready("ncclCommInitRankConfig (communicator bootstrap)");
+  } catch (...) {
+    comm_ = nullptr;  // aborted by wait_ready
+    throw;
   }
   IGG_HIP_CHECK(hipMalloc(&scratch_, 256));
   IGG_HIP_CHECK(hipMemset(scratch_, 0, 256));
@@ -55,7 +76,56 @@ RcclComm::RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank)
 
 RcclComm::~RcclComm() {
   if (scratch_) (void)hipFree(scratch_);
-  if (comm_ && !aborted_) (void)ncclCommDestroy(comm_);
+  if (!comm_ || aborted_) return;
+  // Finalize (flushes outstanding work; non-blocking: polled with a bound),
+  // then destroy; a communicator that cannot finalize is aborted instead.
+  ncclResult_t st = ncclCommFinalize(comm_);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (st == ncclInProgress || st == ncclSuccess) {
+    if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) break;
+    if (st != ncclInProgress) break;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 10.0) break;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  if (st == ncclSuccess) (void)ncclCommDestroy(comm_);
+  else (void)ncclCommAbort(comm_);
+  comm_ = nullptr;
+}
+
+void RcclComm::wait_ready(const char* what) {
+  // Poll the communicator's state until the last call completed (ncclSuccess),
+  // failed, or the deadline passed (then abort: RCCL work waiting on a peer
+  // exits, and every later call raises).
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spins = 0;; ++spins) {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+    if (q != ncclSuccess) st = q;
+    if (st == ncclSuccess) return;
+    if (st != ncclInProgress) {
+      (void)ncclCommAbort(comm_);
+      aborted_ = true;
+      fail("RCCL error '", ncclGetErrorString(st), "' in ", what, " (rank ", rank_, " of ", nranks_, ")");
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_) {
+      (void)ncclCommAbort(comm_);
+      aborted_ = true;
+      fail(what, " did not complete within ", timeout_s_, " s on rank ", rank_, " of ", nranks_,
+           " (a peer rank never arrived?); the RCCL communicator was aborted");
+    }
+    if (spins < 1000) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(500));
+  }
+}
+
+void RcclComm::settle(int result, const char* what) {
+  const ncclResult_t r = static_cast<ncclResult_t>(result);
+  if (r == ncclSuccess) return;
+  if (r == ncclInProgress) {  // non-blocking: a first contact (p2p connection setup) runs in the background
+    wait_ready(what);
+    return;
+  }
+  fail("RCCL error '", ncclGetErrorString(r), "' in ", what);
 }
 
 void RcclComm::exchange(const std::vector<P2POp>& recvs, const std::vector<P2POp>& sends,
@@ -76,12 +146,12 @@ void RcclComm::exchange(const std::vector<P2POp>& recvs, const std::vector<P2POp
     (void)ncclGroupEnd();
     throw;
   }
-  IGG_NCCL_CHECK(ncclGroupEnd());
+  settle(ncclGroupEnd(), "ncclGroupEnd (halo send/recv group)");
 }
 
 void RcclComm::barrier(hipStream_t stream) {
   if (aborted_) fail("RCCL communicator was aborted");
-  IGG_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, stream));
+  settle(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, stream), "ncclAllReduce (barrier)");
 }
 
 namespace {
@@ -119,14 +189,14 @@ ncclRedOp_t nccl_op(int op) {
 void RcclComm::allreduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t stream) {
   if (aborted_) fail("RCCL communicator was aborted");
   if (count == 0) return;
-  IGG_NCCL_CHECK(ncclAllReduce(send, recv, count, nccl_type(dtype), nccl_op(op), comm_, stream));
+  settle(ncclAllReduce(send, recv, count, nccl_type(dtype), nccl_op(op), comm_, stream), "ncclAllReduce");
 }
 
 void RcclComm::broadcast(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t stream) {
   if (aborted_) fail("RCCL communicator was aborted");
   if (root < 0 || root >= nranks_) fail("RcclComm.broadcast: root ", root, " out of range");
   if (count == 0) return;
-  IGG_NCCL_CHECK(ncclBroadcast(send, recv, count, nccl_type(dtype), root, comm_, stream));
+  settle(ncclBroadcast(send, recv, count, nccl_type(dtype), root, comm_, stream), "ncclBroadcast");
 }
 
 void RcclComm::check_async_error() {

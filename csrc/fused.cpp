@@ -107,15 +107,19 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
   if (a.elem_bytes != elem_) fail("FusedHalo.step: field dtype does not match the fused halo");
   if (entry) sync(stream);  // entry barrier (fused.hpp)
   HaloIOArgs x = io(step, primed, a.t2, (mode & 4) != 0);
-  // Step synchronisation inside the kernel (put.hpp StepSync), else the sync
-  // kernel after it (IGG_FUSED_SYNC_KERNEL=1, or a launch that cannot count
-  // its exchanging waves).
+  // Step synchronisation: the 1-wave sync kernel after the stencil (default:
+  // rehearsed with 8 ranks, and as fast as the in-kernel form,
+  // profiles/r3_boxes/), or inside the kernel (put.hpp StepSync) with send
+  // mode bit 16 - a separately validated candidate of the bench's A/B, never
+  // where ranks share a GPU (its waiting waves can hold the CUs a co-resident
+  // rank's kernel needs: the forced 8-rank shared-GPU rehearsal timed out).
+  // IGG_FUSED_SYNC_KERNEL / set_step_sync override both.
   bool used = false;
-  if (in_kernel_sync() && sync_.n_out > 0) {  // no neighbour: nothing to synchronise in the kernel
+  if (in_kernel_sync(mode) && sync_.n_out > 0) {  // no neighbour: nothing to synchronise in the kernel
     x.sync = step_sync_from(sync_);
     x.sync_used = &used;
   }
-  launch_diffusion3d_fused(a, x, variant, mode, stream);
+  launch_diffusion3d_fused(a, x, variant, mode & 15, stream);
   if (!used) sync(stream);
   open_ = used;
 }
@@ -127,8 +131,9 @@ void FusedHalo::drain(hipStream_t stream) {
   open_ = false;
 }
 
-bool FusedHalo::in_kernel_sync() const {
-  return sync_mode_ < 0 ? step_sync_in_kernel(mesh_->shares_device()) : sync_mode_ == 0;
+bool FusedHalo::in_kernel_sync(int mode) const {
+  if (sync_mode_ >= 0) return sync_mode_ == 0;
+  return step_sync_in_kernel(mesh_->shares_device(), (mode & IN_KERNEL_SYNC) != 0);
 }
 
 }  // namespace igg

@@ -1,5 +1,6 @@
 // Device gather-to-root (see include/igg/gather.hpp).
 #include "igg/gather.hpp"
+#include "igg/fault.hpp"
 #include "igg/trace.hpp"
 #include "igg/ipc.hpp"
 
@@ -108,8 +109,9 @@ PullGatherer::~PullGatherer() {
   for (auto& per : mapped_)
     for (auto& m : per)
       if (m.second) (void)hipIpcCloseMemHandle(m.second);
-  if (!stage_.empty()) (void)hipDeviceSynchronize();
+  if (!stage_.empty() || !retired_.empty()) (void)hipDeviceSynchronize();
   for (char* c : stage_) (void)hipFree(c);
+  for (char* c : retired_) (void)hipFree(c);
   for (hipEvent_t& e : peer_ev_)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : root_done_)
@@ -140,9 +142,11 @@ void PullGatherer::free() {
       if (m.second) (void)hipIpcCloseMemHandle(m.second);
     per.clear();
   }
-  if (!stage_.empty()) IGG_HIP_CHECK(hipDeviceSynchronize());
+  if (!stage_.empty() || !retired_.empty()) IGG_HIP_CHECK(hipDeviceSynchronize());
   for (char* c : stage_) IGG_HIP_CHECK(hipFree(c));
+  for (char* c : retired_) IGG_HIP_CHECK(hipFree(c));
   stage_.clear();
+  retired_.clear();
   stage_bytes_ = 0;
 }
 
@@ -156,142 +160,177 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
   ensure_streams();
   const size_t EH = sizeof(hipIpcEventHandle_t), MH = sizeof(hipIpcMemHandle_t);
   const size_t plane = static_cast<size_t>(a.size[1] * a.size[2]) * a.elem_bytes;
-  std::string rec;  // after the event handle: 'D' handle offset | 'C' nchunks planes/chunk handles...
-  if (rank_ != root) {
-    void* base = nullptr;
-    size_t size = 0;
-    IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(a.ptr)));
-    bool forced = false;
-    const size_t cap = chunk_cap(&forced);
-    if (size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
-      // Stage into exportable chunks of whole planes (class comment).
-      const int64_t ppc = std::max<int64_t>(1, static_cast<int64_t>(cap / std::max<size_t>(plane, 1)));
-      const size_t cb = static_cast<size_t>(ppc) * plane;
-      if (cb >= IPC_MAX_BYTES) fail("gather_async: one x-plane of the local array exceeds the IPC limit");
-      const int64_t nch = (a.size[0] + ppc - 1) / ppc;
-      if (stage_bytes_ < cb || static_cast<int64_t>(stage_.size()) < nch) {
-        IGG_HIP_CHECK(hipDeviceSynchronize());  // rare (grow-only): no pull of the old chunks in flight
-        for (char* c : stage_) IGG_HIP_CHECK(hipFree(c));
-        stage_.clear();
-        for (int64_t k = 0; k < nch; ++k) {
-          char* c = nullptr;
-          IGG_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c), cb));
-          stage_.push_back(c);
+  // Every rank prepares its record (export handles, staged chunks) and joins
+  // the allgather whatever happens: a rank that failed sends status '0' and
+  // its error, so every rank raises together instead of the others blocking
+  // in a collective (as PeerMesh::map_buffers does).
+  std::string mine(1, '1'), error;
+  try {
+    inject_fail("gather_export");
+    std::string rec;  // after the event handle: 'D' handle offset | 'C' nchunks planes/chunk handles...
+    if (rank_ != root) {
+      void* base = nullptr;
+      size_t size = 0;
+      IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(a.ptr)));
+      bool forced = false;
+      const size_t cap = chunk_cap(&forced);
+      if (size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
+        // Stage into exportable chunks of whole planes (class comment).
+        const int64_t ppc = std::max<int64_t>(1, static_cast<int64_t>(cap / std::max<size_t>(plane, 1)));
+        const size_t cb = static_cast<size_t>(ppc) * plane;
+        if (cb >= IPC_MAX_BYTES) fail("gather_async: one x-plane of the local array exceeds the IPC limit");
+        const int64_t nch = (a.size[0] + ppc - 1) / ppc;
+        if (stage_bytes_ < cb || static_cast<int64_t>(stage_.size()) < nch) {
+          // Rare (grow-only). The grown-out chunks are RETIRED, not freed,
+          // until free(): an IPC export of a new allocation at a freed one's
+          // address was seen to map the OLD memory in the peer
+          // (profiles/r3_put_arena/), so every export address stays new and
+          // the root, seeing new handles, re-maps.
+          for (char* c : stage_) retired_.push_back(c);
+          stage_.clear();
+          for (int64_t k = 0; k < nch; ++k) {
+            char* c = nullptr;
+            IGG_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c), cb));
+            stage_.push_back(c);
+          }
+          stage_bytes_ = cb;
         }
-        stage_bytes_ = cb;
+        rec.push_back('C');
+        put_u32(rec, static_cast<uint32_t>(nch));
+        put_u32(rec, static_cast<uint32_t>(ppc));
+        for (int64_t k = 0; k < nch; ++k) {
+          const int64_t nx = std::min<int64_t>(ppc, a.size[0] - k * ppc);
+          IGG_HIP_CHECK(hipMemcpyAsync(stage_[k], reinterpret_cast<const char*>(a.ptr) + k * ppc * plane,
+                                       static_cast<size_t>(nx) * plane, hipMemcpyDeviceToDevice, stream));
+          rec += ipc_get_handle(stage_[k]);
+        }
+      } else {
+        const uint64_t off = a.ptr - reinterpret_cast<uintptr_t>(base);
+        rec.push_back('D');
+        rec += ipc_get_handle(base);
+        rec.append(reinterpret_cast<const char*>(&off), sizeof(off));
       }
-      rec.push_back('C');
-      put_u32(rec, static_cast<uint32_t>(nch));
-      put_u32(rec, static_cast<uint32_t>(ppc));
-      for (int64_t k = 0; k < nch; ++k) {
-        const int64_t nx = std::min<int64_t>(ppc, a.size[0] - k * ppc);
-        IGG_HIP_CHECK(hipMemcpyAsync(stage_[k], reinterpret_cast<const char*>(a.ptr) + k * ppc * plane,
-                                     static_cast<size_t>(nx) * plane, hipMemcpyDeviceToDevice, stream));
-        rec += ipc_get_handle(stage_[k]);
+    }
+    // `a` (or its staged copy; on the root also dst) is final where the
+    // caller's stream has got to now: an interprocess event marks that point
+    // (no host drain).
+    IGG_HIP_CHECK(hipEventRecord(ready_, stream));
+    hipIpcEventHandle_t eh;
+    IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, ready_));
+    mine.append(reinterpret_cast<const char*>(&eh), EH);
+    mine += rec;
+    if (rank_ == root) {
+      for (hipEvent_t e : done_) {  // the peers order their streams after these in wait()
+        IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, e));
+        mine.append(reinterpret_cast<const char*>(&eh), EH);
       }
-    } else {
-      const uint64_t off = a.ptr - reinterpret_cast<uintptr_t>(base);
-      rec.push_back('D');
-      rec += ipc_get_handle(base);
-      rec.append(reinterpret_cast<const char*>(&off), sizeof(off));
     }
-  }
-  // `a` (or its staged copy; on the root also dst) is final where the
-  // caller's stream has got to now: an interprocess event marks that point
-  // (no host drain).
-  IGG_HIP_CHECK(hipEventRecord(ready_, stream));
-  hipIpcEventHandle_t eh;
-  IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, ready_));
-  std::string mine(reinterpret_cast<const char*>(&eh), EH);
-  mine += rec;
-  if (rank_ == root) {
-    for (hipEvent_t e : done_) {  // the peers order their streams after these in wait()
-      IGG_HIP_CHECK(hipIpcGetEventHandle(&eh, e));
-      mine.append(reinterpret_cast<const char*>(&eh), EH);
-    }
+  } catch (const Error& e) {
+    error = e.what();
+    mine.assign("0");
+    mine += error;
   }
   // Host rendezvous only (every rank has recorded its event before the root
   // waits on it), not a GPU drain.
-  const std::vector<std::string> all = allgather_(mine);
+  std::vector<std::string> all = allgather_(mine);
   if (static_cast<int>(all.size()) != nranks_) fail("gather_async: allgather returned ", all.size(), " entries");
+  for (int r = 0; r < nranks_; ++r)
+    if (all[r].empty() || all[r][0] != '1')
+      fail("gather_async: rank ", r, " could not export its block",
+           all[r].size() > 1 ? std::string(" (") + all[r].substr(1, 300) + ")" : std::string());
+  for (auto& x : all) x.erase(0, 1);
   const int nside = static_cast<int>(side_.size());
   used_ = std::min(nranks_, nside);
-  if (rank_ == root) {
-    // Every copy stream starts behind the root's own stream: its earlier work
-    // on dst (a fill, a previous consumer of a reused allocation) comes first.
-    for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipStreamWaitEvent(side_[k], ready_, 0));
-    for (int p = 0; p < nranks_; ++p) {
-      const Int3 c{p / (dims[1] * dims[2]), (p / dims[2]) % dims[1], p % dims[2]};
-      hipStream_t s = side_[p % nside];
-      const void* src = nullptr;
-      if (p == root) {
-        src = reinterpret_cast<const void*>(a.ptr);
-      } else {
-        const std::string& rec = all[p];
-        if (rec.size() < EH + 1) fail("gather_async: malformed handles from rank ", p);
-        const std::string ekey = rec.substr(0, EH);
-        if (peer_key_[p] != ekey) {  // opened once per peer event
-          if (peer_ev_[p]) IGG_HIP_CHECK(hipEventDestroy(peer_ev_[p]));
-          hipIpcEventHandle_t peh;
-          std::memcpy(&peh, ekey.data(), EH);
-          IGG_HIP_CHECK(hipIpcOpenEventHandle(&peer_ev_[p], peh));
-          peer_key_[p] = ekey;
-        }
-        IGG_HIP_CHECK(hipStreamWaitEvent(s, peer_ev_[p], 0));
-        const char mode = rec[EH];
-        const size_t nbuf = mode == 'C' && rec.size() >= EH + 9 ? get_u32(rec, EH + 1) : 1;
-        const size_t hdr = mode == 'C' ? EH + 9 : EH + 1;
-        if ((mode != 'C' && mode != 'D') || (mode == 'D' && rec.size() != hdr + MH + 8) ||
-            (mode == 'C' && rec.size() != hdr + nbuf * MH))
-          fail("gather_async: malformed handles from rank ", p);
-        auto& per = mapped_[p];
-        bool changed = per.size() != nbuf;
-        for (size_t k = 0; k < nbuf && !changed; ++k) changed = per[k].first != rec.substr(hdr + k * MH, MH);
-        if (changed) {  // this rank's array (or staging) lives in other allocations now
-          if (!per.empty()) {
-            for (hipStream_t q : side_) IGG_HIP_CHECK(hipStreamSynchronize(q));  // rare: old copies drained
-            for (auto& m : per) ipc_close(m.second);
+  // The root maps the blocks and enqueues the pulls; a second status round
+  // tells the peers whether that worked (they would otherwise wait for a
+  // gather that never comes in wait()'s rendezvous).
+  std::string status("1");
+  try {
+    if (rank_ == root) {
+      // Every copy stream starts behind the root's own stream: its earlier work
+      // on dst (a fill, a previous consumer of a reused allocation) comes first.
+      for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipStreamWaitEvent(side_[k], ready_, 0));
+      for (int p = 0; p < nranks_; ++p) {
+        const Int3 c{p / (dims[1] * dims[2]), (p / dims[2]) % dims[1], p % dims[2]};
+        hipStream_t s = side_[p % nside];
+        const void* src = nullptr;
+        if (p == root) {
+          src = reinterpret_cast<const void*>(a.ptr);
+        } else {
+          const std::string& rec = all[p];
+          if (rec.size() < EH + 1) fail("gather_async: malformed handles from rank ", p);
+          const std::string ekey = rec.substr(0, EH);
+          if (peer_key_[p] != ekey) {  // opened once per peer event
+            if (peer_ev_[p]) IGG_HIP_CHECK(hipEventDestroy(peer_ev_[p]));
+            hipIpcEventHandle_t peh;
+            std::memcpy(&peh, ekey.data(), EH);
+            IGG_HIP_CHECK(hipIpcOpenEventHandle(&peer_ev_[p], peh));
+            peer_key_[p] = ekey;
           }
-          per.clear();
-          for (size_t k = 0; k < nbuf; ++k) {
-            const std::string key = rec.substr(hdr + k * MH, MH);
-            per.emplace_back(key, ipc_open(key));
+          IGG_HIP_CHECK(hipStreamWaitEvent(s, peer_ev_[p], 0));
+          const char mode = rec[EH];
+          const size_t nbuf = mode == 'C' && rec.size() >= EH + 9 ? get_u32(rec, EH + 1) : 1;
+          const size_t hdr = mode == 'C' ? EH + 9 : EH + 1;
+          if ((mode != 'C' && mode != 'D') || (mode == 'D' && rec.size() != hdr + MH + 8) ||
+              (mode == 'C' && rec.size() != hdr + nbuf * MH))
+            fail("gather_async: malformed handles from rank ", p);
+          auto& per = mapped_[p];
+          bool changed = per.size() != nbuf;
+          for (size_t k = 0; k < nbuf && !changed; ++k) changed = per[k].first != rec.substr(hdr + k * MH, MH);
+          if (changed) {  // this rank's array (or staging) lives in other allocations now
+            if (!per.empty()) {
+              for (hipStream_t q : side_) IGG_HIP_CHECK(hipStreamSynchronize(q));  // rare: old copies drained
+              for (auto& m : per) ipc_close(m.second);
+            }
+            per.clear();
+            inject_fail("gather_open");
+            for (size_t k = 0; k < nbuf; ++k) {
+              const std::string key = rec.substr(hdr + k * MH, MH);
+              per.emplace_back(key, ipc_open(key));
+            }
           }
-        }
-        if (mode == 'C') {
-          const int64_t ppc = get_u32(rec, EH + 5);
-          for (size_t k = 0; k < nbuf; ++k) {
-            const int64_t x0 = static_cast<int64_t>(k) * ppc;
-            copy_block(per[k].second, dst, a.size, dims, c, x0, std::min<int64_t>(ppc, a.size[0] - x0),
-                       a.elem_bytes, s);
+          if (mode == 'C') {
+            const int64_t ppc = get_u32(rec, EH + 5);
+            for (size_t k = 0; k < nbuf; ++k) {
+              const int64_t x0 = static_cast<int64_t>(k) * ppc;
+              copy_block(per[k].second, dst, a.size, dims, c, x0, std::min<int64_t>(ppc, a.size[0] - x0),
+                         a.elem_bytes, s);
+            }
+            continue;
           }
-          continue;
+          uint64_t off = 0;
+          std::memcpy(&off, rec.data() + hdr + MH, 8);
+          src = static_cast<const char*>(per[0].second) + off;
         }
-        uint64_t off = 0;
-        std::memcpy(&off, rec.data() + hdr + MH, 8);
-        src = static_cast<const char*>(per[0].second) + off;
+        copy_block(src, dst, a.size, dims, c, 0, a.size[0], a.elem_bytes, s);
       }
-      copy_block(src, dst, a.size, dims, c, 0, a.size[0], a.elem_bytes, s);
-    }
-    for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipEventRecord(done_[k], side_[k]));
-  } else {
-    const std::string& rec = all[root];
-    if (rec.size() != EH * (1 + used_)) fail("gather_async: malformed handles from the root");
-    if (static_cast<int>(root_done_.size()) < used_) {
-      root_done_.resize(used_, nullptr);
-      root_key_.resize(used_);
-    }
-    for (int k = 0; k < used_; ++k) {
-      const std::string key = rec.substr(EH * (1 + k), EH);
-      if (root_key_[k] != key) {
-        if (root_done_[k]) IGG_HIP_CHECK(hipEventDestroy(root_done_[k]));
-        hipIpcEventHandle_t h;
-        std::memcpy(&h, key.data(), EH);
-        IGG_HIP_CHECK(hipIpcOpenEventHandle(&root_done_[k], h));
-        root_key_[k] = key;
+      for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipEventRecord(done_[k], side_[k]));
+    } else {
+      const std::string& rec = all[root];
+      if (rec.size() != EH * (1 + used_)) fail("gather_async: malformed handles from the root");
+      if (static_cast<int>(root_done_.size()) < used_) {
+        root_done_.resize(used_, nullptr);
+        root_key_.resize(used_);
+      }
+      for (int k = 0; k < used_; ++k) {
+        const std::string key = rec.substr(EH * (1 + k), EH);
+        if (root_key_[k] != key) {
+          if (root_done_[k]) IGG_HIP_CHECK(hipEventDestroy(root_done_[k]));
+          hipIpcEventHandle_t h;
+          std::memcpy(&h, key.data(), EH);
+          IGG_HIP_CHECK(hipIpcOpenEventHandle(&root_done_[k], h));
+          root_key_[k] = key;
+        }
       }
     }
+  } catch (const Error& e) {
+    status = std::string("0") + e.what();
   }
+  const std::vector<std::string> st = allgather_(status);
+  for (int r = 0; r < static_cast<int>(st.size()); ++r)
+    if (st[r].empty() || st[r][0] != '1')
+      fail("gather_async: rank ", r, " could not map or pull the blocks",
+           st[r].size() > 1 ? std::string(" (") + st[r].substr(1, 300) + ")" : std::string());
   root_ = root;
   pending_ = true;
 }

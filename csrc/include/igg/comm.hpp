@@ -49,7 +49,11 @@ class RcclComm : public Transport {
  public:
   static constexpr size_t UID_BYTES = 128;
   static std::vector<uint8_t> unique_id();
-  RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank);
+  // Bounded bootstrap: a non-blocking communicator polled for at most
+  // `timeout_s` seconds (<= 0: first_contact_timeout(), IGG_FIRST_CONTACT_TIMEOUT);
+  // on expiry it is aborted and igg::Error raised. Callers make the outcome
+  // collective (parallel/comm.py ensure_rccl: every rank raises together).
+  RcclComm(const std::vector<uint8_t>& uid, int nranks, int rank, double timeout_s = 0);
   ~RcclComm() override;
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -81,6 +85,12 @@ class RcclComm : public Transport {
   int rank_ = 0, nranks_ = 1;
   void* scratch_ = nullptr;  // device int for the barrier
   bool aborted_ = false;
+  double timeout_s_ = 120.0;
+  // Non-blocking communicator: a call that returned ncclInProgress (the
+  // bootstrap, a first p2p contact's connection setup) is polled until it
+  // completes, fails, or timeout_s_ passes (then the communicator is aborted).
+  void wait_ready(const char* what);
+  void settle(int result, const char* what);
 };
 
 std::string rccl_version();

@@ -8,12 +8,13 @@
 // (launch_diffusion3d_fused) stores, while sweeping the interior, the planes
 // each neighbour needs (x=1/n0-2, y=1/n1-2, z=1/n2-2) into that neighbour's
 // IPC-mapped, fine-grained arena with system-scope stores (st_sys), and reads
-// its own face halos from its arena instead of from the field. Its exchanging
-// waves also synchronise the step with the neighbours (put.hpp StepSync: wait
-// for the neighbours' previous step, the last one publishes this step; bounded
-// spins, error flag on timeout). Where another rank shares the GPU, or with
-// IGG_FUSED_SYNC_KERNEL=1, a 1-wave sync kernel after the stencil does that
-// instead (waiting waves could hold the compute units the other rank needs).
+// its own face halos from its arena instead of from the field. A 1-wave sync
+// kernel after the stencil synchronises the step with the neighbours (publish
+// "arrived", wait for theirs; bounded spins, error flag on timeout). With send
+// mode bit 16 the exchanging waves do that inside the stencil instead
+// (put.hpp StepSync: wait for the neighbours' previous step, the last one
+// publishes this step) - not where another rank shares the GPU (waiting waves
+// could hold the compute units the other rank needs).
 // The arena has two halves: step i writes half i&1 and reads half (i-1)&1, so
 // a neighbour may run one step ahead without overwriting data still in use;
 // the per-step neighbour synchronisation bounds the skew to one.
@@ -91,7 +92,10 @@ class FusedHalo {
   // sync kernel after it: -1 the default (step_sync_in_kernel), 0 in the
   // kernel, 1 sync kernel. Every rank must use the same form.
   void set_step_sync(int mode) { sync_mode_ = mode; }
-  bool in_kernel_sync() const;
+  // Send mode bit selecting the in-kernel step synchronisation (step()).
+  static constexpr int IN_KERNEL_SYNC = 16;
+  // Whether a step with send mode `mode` synchronises inside the kernel.
+  bool in_kernel_sync(int mode = 0) const;
 
   int64_t region_offset(int d, int s) const { return off_[d][s]; }  // elements within a half
   int64_t half_elems() const { return half_; }

@@ -102,6 +102,7 @@ class PullGatherer {
   std::vector<std::vector<std::pair<std::string, void*>>> mapped_;
   std::vector<char*> stage_;  // own staging chunks (a large `a`), grow-only
   size_t stage_bytes_ = 0;    // bytes of each staging chunk
+  std::vector<char*> retired_;  // grown-out staging chunks, freed at free() (never re-exported addresses)
   bool pending_ = false;
   int root_ = 0;
   int used_ = 0;  // copy streams used by the pending gather

@@ -79,11 +79,12 @@ StepSync step_sync_from(const PutSync& s);
 // IGG_FUSED_SYNC_KERNEL unset: `by_default` unless another rank of the mesh
 // shares this rank's GPU (its waiting waves could starve that rank's kernel);
 // "1": never (the sync kernel after every step); "0": always (tests whose
-// kernels cannot fill the GPU). FusedHalo passes by_default = true; the
+// kernels cannot fill the GPU). FusedHalo passes by_default = send mode bit 16
+// (an A/B candidate of its own; the sync kernel is the default); the
 // acoustic step false: its ~8,300 exchanging waves per 8192^2 step each count
 // themselves with one atomic on the same uncached word, and those serialise
 // (0.70-0.75 vs 0.306 ms/step with the sync kernel, profiles/r3_stepsync/).
-bool step_sync_in_kernel(bool shares_device, bool by_default = true);
+bool step_sync_in_kernel(bool shares_device, bool by_default);
 
 void launch_put_begin(const PutSync& s, hipStream_t stream);
 void launch_put_sync(const PutSync& s, hipStream_t stream);

@@ -2,6 +2,8 @@
 
 #include <cstring>
 
+#include "igg/fault.hpp"
+
 namespace igg {
 
 void* ipc_malloc(size_t bytes, MemKind kind) {
@@ -45,9 +47,20 @@ void* ipc_open(const std::string& handle) {
     fail("ipc_open: handle has ", handle.size(), " bytes, expected ", sizeof(hipIpcMemHandle_t));
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle.data(), sizeof(h));
-  void* p = nullptr;
-  IGG_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  return p;
+  // First contact with a peer's memory: bounded (fault.hpp). This runtime has
+  // been seen to never return from an open (allocations of 2 GiB or more,
+  // profiles/r3_ipc/); a stuck open must fail the mesh on every rank, not hang
+  // the job.
+  auto p = std::make_shared<void*>(nullptr);
+  run_bounded(
+      [p, h]() {
+        inject_delay("ipc_open");
+        void* q = nullptr;
+        IGG_HIP_CHECK(hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess));
+        *p = q;
+      },
+      first_contact_timeout(), "hipIpcOpenMemHandle (mapping a peer's memory)");
+  return *p;
 }
 
 void ipc_close(void* p) {

@@ -47,6 +47,11 @@ NNEIGHBORS = int(native.NNEIGHBORS)
 ALLOC_GRANULARITY = int(native.ALLOC_GRANULARITY)
 THREADCOPY_THRESHOLD = int(native.THREADCOPY_THRESHOLD)
 
+if os.environ.get("IGG_CRASH_BACKTRACE") == "1":
+    # native backtrace of a fatal signal first, then faulthandler's Python
+    # stack (enable faulthandler before importing igg for the chain)
+    native.install_crash_handler()
+
 
 def native_path() -> str:
     return native.__file__

@@ -109,6 +109,7 @@ class Communicator:
     local_size: int = 1
     _transports: dict = field(default_factory=dict)
     aborted: str = ""
+    rccl_error: str = ""  # a failed RCCL bootstrap (every rank agrees): not retried
 
     def __eq__(self, other):  # identity semantics like MPI.Comm handles
         return self is other
@@ -272,10 +273,32 @@ class Communicator:
         return self.all_gather_object(bytes(b))
 
     def ensure_rccl(self):
+        """The grid's native RCCL communicator, created on first use
+        (collective). The bootstrap is bounded (a non-blocking communicator
+        polled for IGG_FIRST_CONTACT_TIMEOUT seconds, then aborted) and its
+        outcome is agreed over gloo: if any rank failed, every rank raises the
+        same IGGError, and later calls raise it again at once instead of
+        re-running a bootstrap that already failed (reference: a failing rank
+        aborts the MPI job, src/init_global_grid.jl:80-92)."""
         if self.rccl is None and self.size > 1:
+            if self.rccl_error:
+                raise IGGError(self.rccl_error)
             uid = native.RcclComm.unique_id() if self.rank == 0 else None
             uid = self.broadcast_object(uid, root=0)
-            self.rccl = native.RcclComm(uid, self.size, self.rank)
+            rc, err = None, ""
+            try:
+                rc = native.RcclComm(uid, self.size, self.rank, config.first_contact_timeout())
+            except Exception as e:  # bounded bootstrap expired, or RCCL refused (e.g. ranks sharing a GPU)
+                err = f"{type(e).__name__}: {e}"
+            errs = self.all_gather_object(err)
+            bad = [r for r, e in enumerate(errs) if e]
+            if bad:
+                if rc is not None:
+                    rc.abort()
+                self.rccl_error = (f"RCCL communicator could not be created (failed on rank(s) {bad}; "
+                                   f"rank {bad[0]}: {errs[bad[0]][:300]})")
+                raise IGGError(self.rccl_error)
+            self.rccl = rc
         return self.rccl
 
     def _ensure_torch_nccl(self):
@@ -286,6 +309,10 @@ class Communicator:
     def _gloo_p2p(self, recvs, sends, device, stream):
         if device:
             raise IGGError("gloo transport cannot move GPU memory.")
+        if config.host_matching() == "ordered":
+            self._ordered_exchange([(_host_view(p, n), peer) for p, n, peer, _t in recvs],
+                                   [(_host_view(p, n), peer) for p, n, peer, _t in sends])
+            return
         reqs = []
         for ptr, nbytes, peer, tag in recvs:
             reqs.append(dist.irecv(_host_view(ptr, nbytes), src=self.global_rank(peer), group=self.gloo, tag=tag))
@@ -293,6 +320,50 @@ class Communicator:
             reqs.append(dist.isend(_host_view(ptr, nbytes), dst=self.global_rank(peer), group=self.gloo, tag=tag))
         for r in reqs:
             r.wait()
+
+    def _ordered_exchange(self, recvs, sends) -> None:
+        """Order-only point-to-point phase over gloo: the messages of a phase
+        to one peer travel as ONE tag-0 message, concatenated in issue order,
+        and the receiver splits its single message from that peer over its
+        receives in ITS issue order. Nothing but the position pairs the k-th
+        send to a peer with the peer's k-th receive from this rank - exactly
+        RCCL's matching of grouped ncclSend/ncclRecv, and MPI's with every tag
+        0 as in the reference (update_halo.jl:713-735; SURVEY invariant 4:
+        with dims=2 periodic both sides' messages go to ONE peer, and only the
+        right-then-left receive / left-then-right send order makes them land
+        in the right halo). ``recvs``/``sends``: [(uint8 CPU tensor, peer)].
+        IGG_DEBUG_SWAP_SENDS=1 reverses each peer's send order (a test hook:
+        the halo tests must then fail)."""
+        by_s, by_r = {}, {}
+        for t, p in sends:
+            by_s.setdefault(p, []).append(t)
+        for t, p in recvs:
+            by_r.setdefault(p, []).append(t)
+        if os.environ.get("IGG_DEBUG_SWAP_SENDS") == "1":
+            for ts in by_s.values():
+                ts.reverse()
+        reqs, rbuf = [], {}
+        for p, ts in by_r.items():
+            n = sum(t.numel() for t in ts)
+            if n == 0:
+                continue
+            b = ts[0] if len(ts) == 1 else torch.empty(n, dtype=torch.uint8)
+            rbuf[p] = b
+            reqs.append(dist.irecv(b, src=self.global_rank(p), group=self.gloo, tag=0))
+        for p, ts in by_s.items():
+            n = sum(t.numel() for t in ts)
+            if n == 0:
+                continue
+            b = ts[0] if len(ts) == 1 else torch.cat(ts)
+            reqs.append(dist.isend(b, dst=self.global_rank(p), group=self.gloo, tag=0))
+        for r in reqs:
+            r.wait()
+        for p, ts in by_r.items():
+            if len(ts) > 1 and p in rbuf:
+                o = 0
+                for t in ts:
+                    t.copy_(rbuf[p][o:o + t.numel()])
+                    o += t.numel()
 
     def _pinned(self, role: str, k: int, n: int) -> torch.Tensor:
         """Grow-only page-locked host staging buffer (reference: registered host
@@ -313,10 +384,13 @@ class Communicator:
             native.memcpy_d2h_stream(h.data_ptr(), p, n, stream)
             hs.append((h, peer, tag))
         hr = [(self._pinned("r", k, n), p, peer, tag) for k, (p, n, peer, tag) in enumerate(recvs)]
-        reqs = [dist.irecv(h, src=self.global_rank(peer), group=self.gloo, tag=tag) for h, _p, peer, tag in hr]
-        reqs += [dist.isend(h, dst=self.global_rank(peer), group=self.gloo, tag=tag) for h, peer, tag in hs]
-        for r in reqs:
-            r.wait()
+        if config.host_matching() == "ordered":
+            self._ordered_exchange([(h, peer) for h, _p, peer, _t in hr], [(h, peer) for h, peer, _t in hs])
+        else:
+            reqs = [dist.irecv(h, src=self.global_rank(peer), group=self.gloo, tag=tag) for h, _p, peer, tag in hr]
+            reqs += [dist.isend(h, dst=self.global_rank(peer), group=self.gloo, tag=tag) for h, peer, tag in hs]
+            for r in reqs:
+                r.wait()
         for h, p, _peer, _tag in hr:
             native.memcpy_h2d_stream(p, h.data_ptr(), h.numel(), stream)
 

@@ -119,3 +119,24 @@ def gather_pull(env: Mapping[str, str] | None = None) -> bool:
     buffer of nprocs*|A|, no reorder pass); 0 = RCCL receives + reorder kernel."""
     env = os.environ if env is None else env
     return env.get("IGG_GATHER_PULL", "1").strip() not in ("0", "false", "no")
+
+
+def first_contact_timeout(env: Mapping[str, str] | None = None) -> float:
+    """``IGG_FIRST_CONTACT_TIMEOUT``: seconds a first-contact call of the
+    multi-GPU path may take - the RCCL bootstrap, mapping a peer's memory over
+    IPC (default 120). On expiry the call is abandoned and every rank raises
+    together (csrc/include/igg/fault.hpp)."""
+    env = os.environ if env is None else env
+    return float(env.get("IGG_FIRST_CONTACT_TIMEOUT", "120"))
+
+
+def host_matching(env: Mapping[str, str] | None = None) -> str:
+    """``IGG_HOST_MATCHING``: how the host (gloo) paths pair messages.
+    ``ordered`` (default): order-only, like RCCL and the reference's tag-0 MPI
+    messages - one message per peer and phase, paired by issue position;
+    ``tagged``: one message per halo face, paired by a per-face tag."""
+    env = os.environ if env is None else env
+    m = env.get("IGG_HOST_MATCHING", "ordered").strip().lower()
+    if m not in ("ordered", "tagged"):
+        raise ValueError(f"IGG_HOST_MATCHING must be 'ordered' or 'tagged' (got {m!r})")
+    return m

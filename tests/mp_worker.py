@@ -1,4 +1,5 @@
 """Per-rank test scenarios (launched by tests/_mp.py, one process per rank)."""
+import math
 import os
 import sys
 
@@ -103,6 +104,51 @@ def scenario_gather(dev, dt):
         igg.gather_(A, G, root=root)
     igg.finalize_global_grid()
     print(f"rank {me} gather OK")
+
+
+def scenario_gather_regrow():
+    """gather_ (IPC pull of staged chunks, IGG_GATHER_CHUNK_BYTES set by the
+    test) of blocks whose chunks are MiB-sized dedicated allocations and grow
+    between gathers: the grown-out chunks are retired, not freed, so no new
+    export reuses an address the root still has mapped (ADVICE r3:
+    gather.cpp:174); every gathered block is checked."""
+    _device("gpu")
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 8, 8, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    for k, shape in enumerate([(8, 256, 256), (8, 512, 512), (8, 256, 256), (6, 768, 512)]):
+        A = (torch.arange(math.prod(shape), dtype=torch.float64).view(shape) + 1e7 * (me + 1) + 1e9 * k).cuda()
+        G = (torch.zeros(dims[0] * shape[0], dims[1] * shape[1], dims[2] * shape[2], dtype=torch.float64).cuda()
+             if me == 0 else None)
+        igg.gather_(A, G, root=0)
+        if me == 0:
+            Gc = G.cpu()
+            for p in range(nprocs):
+                c = igg.native.cart_coords(p, dims.tolist())
+                blk = Gc[c[0] * shape[0]:(c[0] + 1) * shape[0], c[1] * shape[1]:(c[1] + 1) * shape[1],
+                         c[2] * shape[2]:(c[2] + 1) * shape[2]]
+                exp = torch.arange(math.prod(shape), dtype=torch.float64).view(shape) + 1e7 * (p + 1) + 1e9 * k
+                assert torch.equal(blk, exp), f"gather {k} {shape}: block of rank {p} wrong"
+        del A, G
+    igg.finalize_global_grid()
+    print(f"rank {me} gather regrow OK")
+
+
+def scenario_gather_fail(expect):
+    """IGG_INJECT_FAIL makes one rank's export (or the root's mapping) fail:
+    every rank must raise, none may hang in the collective."""
+    _device("gpu")
+    me, dims, nprocs, coords, comm = igg.init_global_grid(6, 5, 4, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    A = torch.full((6, 5, 4), float(me), dtype=torch.float64, device="cuda")
+    G = torch.zeros(dims[0] * 6, dims[1] * 5, dims[2] * 4, dtype=torch.float64, device="cuda") if me == 0 else None
+    try:
+        igg.gather_(A, G, root=0)
+    except Exception as e:
+        assert expect in str(e), f"rank {me}: unexpected error {e}"
+        print(f"rank {me} raised as expected: {str(e)[:200]}")
+    else:
+        raise AssertionError(f"rank {me}: gather_ did not raise")
+    os._exit(0)  # the failed gather's state is not torn down collectively
 
 
 def scenario_diffusion(dev, nx, ny, nz, steps, overlap):
@@ -607,11 +653,14 @@ def scenario_ring(dev):
                                                           device_type="none" if dev == "cpu" else "AMDGPU")
     gg = igg.get_global_grid()
     left, right = int(gg.neighbors[0, 0]), int(gg.neighbors[1, 0])
-    send = torch.full((16,), float(me), dtype=torch.float64, device=device)
+    # side-distinct payloads: what goes left is me + 0.25, what goes right me + 0.5
+    # (with 2 ranks left == right: only the issue order tells the two apart)
+    send = torch.cat([torch.full((16,), me + 0.25, dtype=torch.float64),
+                      torch.full((16,), me + 0.5, dtype=torch.float64)]).to(device)
     recv = torch.zeros(32, dtype=torch.float64, device=device)
     t = comm.host_transport() if dev == "cpu" else comm.device_transport()
     recvs = [(recv.data_ptr() + 128, 128, right, 1), (recv.data_ptr(), 128, left, 0)]
-    sends = [(send.data_ptr(), 128, left, 1), (send.data_ptr(), 128, right, 0)]
+    sends = [(send.data_ptr(), 128, left, 1), (send.data_ptr() + 128, 128, right, 0)]
     fn = {"gloo": comm._gloo_p2p, "gloo-staged": comm._staged_p2p}.get(t.name)
     stream = torch.cuda.current_stream().cuda_stream if dev != "cpu" else 0
     if fn is not None:
@@ -625,7 +674,7 @@ def scenario_ring(dev):
     if dev != "cpu":
         torch.cuda.synchronize()
     r = recv.cpu()
-    assert (r[:16] == left).all() and (r[16:] == right).all(), f"rank {me}: ring wrong {r}"
+    assert (r[:16] == left + 0.5).all() and (r[16:] == right + 0.25).all(), f"rank {me}: ring wrong {r}"
     igg.finalize_global_grid()
     print(f"rank {me} ring OK")
 

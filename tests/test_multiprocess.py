@@ -50,6 +50,37 @@ def test_ring_cpu():
     run_ranks(3, "ring", "cpu")
 
 
+# --- order-only matching (the default host matching, IGG_HOST_MATCHING=ordered):
+# one tag-0 message per peer and phase, paired with the peer's receives by issue
+# position only - RCCL's rule, and MPI's with the reference's all-zero tags
+# (update_halo.jl:713-735). A tagged transport would mask an ordering bug
+# between two distinct ranks; these runs would not.
+@pytest.mark.parametrize("nprocs", [2, 3])
+def test_ring_cpu_order_only(nprocs):
+    run_ranks(nprocs, "ring", "cpu", env_extra={"IGG_HOST_MATCHING": "ordered"})
+
+
+@pytest.mark.parametrize("matching", ["ordered", "tagged"])
+def test_halo_cpu_matching_forms_agree(matching):
+    run_ranks(2, "halo", "cpu", 7, 5, 6, 1, 1, 1, "f64",
+              env_extra={"IGG_HOST_MATCHING": matching, "IGG_HALO_MODE": "sequential"})
+
+
+@pytest.mark.parametrize("scenario,args,mode", [
+    ("halo", (7, 5, 6, 1, 1, 1, "f64"), "sequential"),  # dims=2 periodic: both x faces go to ONE peer
+    ("halo", (7, 5, 6, 1, 1, 1, "f64"), "onephase"),
+    ("ring", (), None),
+])
+def test_order_only_matching_catches_a_swapped_send_order(scenario, args, mode):
+    """The same runs with every peer's sends issued in reverse order
+    (IGG_DEBUG_SWAP_SENDS=1) must fail: nothing but the order pairs them."""
+    env = {"IGG_HOST_MATCHING": "ordered", "IGG_DEBUG_SWAP_SENDS": "1"}
+    if mode:
+        env["IGG_HALO_MODE"] = mode
+    with pytest.raises(AssertionError):
+        run_ranks(2, scenario, "cpu", *args, env_extra=env, timeout=60)
+
+
 # --- same scenarios with GPU fields, several ranks sharing the one GPU via the
 # host-staged transport (exercises the HIP pack/unpack kernels across ranks).
 GPU_ENV = {"IGG_TRANSPORT": "staged"}
@@ -123,6 +154,22 @@ def test_gather_pull_staged_chunks_gpu(nprocs):
     pulled chunk by chunk: gather_async_ (ordering, reuse) and gather_."""
     run_ranks(nprocs, "gather_async", env_extra=dict(PUT_ENV, IGG_GATHER_CHUNK_BYTES="400"))
     run_ranks(nprocs, "gather", "gpu", "f64", env_extra=dict(PUT_ENV, IGG_GATHER_CHUNK_BYTES="100"))
+
+
+@pytest.mark.gpu
+def test_gather_pull_chunk_regrowth_gpu():
+    """Staged chunks of MiB size (dedicated allocations) that grow between
+    gathers are retired, not freed: every gathered block stays right."""
+    run_ranks(3, "gather_regrow", env_extra=dict(PUT_ENV, IGG_GATHER_CHUNK_BYTES=str(1 << 20)), timeout=160)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inject,expect", [("gather_export@1", "could not export"),
+                                           ("gather_open@0", "could not map or pull")])
+def test_gather_pull_failure_is_collective_gpu(inject, expect):
+    """A rank whose export fails (or a root whose mapping fails) does not leave
+    the others blocked in the gather's collective: every rank raises."""
+    run_ranks(3, "gather_fail", expect, env_extra=dict(PUT_ENV, IGG_INJECT_FAIL=inject), timeout=120)
 
 
 # --- fused halo exchange (stencil kernel stores into the neighbours' arenas)
