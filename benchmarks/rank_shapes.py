@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Fused-exchange cost per RANK SHAPE of a real node (1 GPU, self as peer).
+
+The round-3 ratios (1.05x) were measured on an emulated INTERIOR rank (six
+faces). An 8-GPU node runs 2x1x1 / 2x2x1 / 2x2x2 decompositions without
+periodicity, where every rank has ONE neighbour per split dimension, on the
+high side (coordinate 0) or the low side (coordinate 1). This script times,
+for each such one-sided shape (and the six-face interior for reference):
+
+  plain   the best plain stencil (variants x grid rounds), no exchange;
+  fused   each fused candidate of the bench's A/B (variant / send mode /
+          rounds, incl. direct z and peeled x planes), stencil + sync kernel,
+
+all in the time loop's ping-pong shape (T2 = f(T), T = f(T2)), interleaved,
+median of rounds. The exchange partner is this rank itself (a one-sided
+shape stores into its own arena / fields and reads halos nobody wrote:
+timing only, the values are not checked here - tests/test_fused.py checks
+them). ratio = best fused / best plain.
+
+Usage: python benchmarks/rank_shapes.py [--n 512] [--dtype float64]
+       [--shapes x+,x-,xy+,xy-,xyz+,xyz-,xyz] [--steps 20] [--rounds 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import igg  # noqa: E402
+from igg._native import native  # noqa: E402
+
+PLAIN = (0, 2, 9, 11, 14, 24, 25, 40, 43)
+ROUNDS = (1, 2, 3)
+# bench.py FUSED_CANDIDATES / FUSED_DIRECT / FUSED_DIRECT_F32 (+ peel bit 8)
+FUSED = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (9, 0, 3), (14, 0, 3), (40, 0, 2), (42, 0, 2), (42, 1, 2), (50, 0, 2),
+         (11, 0, 2), (11, 2, 2), (11, 8, 2), (11, 10, 2), (14, 0, 2), (9, 0, 2))
+DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
+DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4))
+
+
+def neighbours(shape: str):
+    """nb[d] = [low, high] (0 = this rank, -1 = none) of a named shape."""
+    dims = shape.rstrip("+-")
+    side = shape[len(dims):] or "+-"
+    nb = []
+    for d in "xyz":
+        if d in dims:
+            nb.append([0 if "-" in side else -1, 0 if "+" in side else -1])
+        else:
+            nb.append([-1, -1])
+    return nb
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--shapes", default="x+,x-,xy+,xy-,xyz+,xyz-,xyz")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--candidates", default=None, help="v/mode/rounds,... (default: the bench's lists)")
+    ap.add_argument("--json", default=None, help="write the results here")
+    ap.add_argument("--inkernel", type=int, default=3,
+                    help="re-time the N fastest forms per shape with the in-kernel step sync (send mode bit 16)")
+    a = ap.parse_args()
+    n = a.n
+    dt = getattr(torch, a.dtype)
+    igg.init_global_grid(n, n, n, periodx=1, periody=1, periodz=1, quiet=True)
+    from igg.models.diffusion3d import native_buffer
+
+    # fine-grained fields in one allocation, as the model allocates them
+    nbytes = n * n * n * dt.itemsize
+    buf = native_buffer(3 * nbytes + 2 * 266240, 1, torch.device("cuda", 0))
+    T, T2, Cp = (buf[k * (nbytes + 266240):k * (nbytes + 266240) + nbytes].view(dt).view(n, n, n) for k in range(3))
+    g = torch.Generator(device="cpu").manual_seed(0)
+    T.copy_(torch.rand(n, n, n, generator=g, dtype=torch.float64).to(dt))
+    T2.copy_(T)
+    Cp.copy_(torch.rand(n, n, n, generator=g, dtype=torch.float64).to(dt) + 1)
+    rd2 = [1.0, 1.0, 1.0]
+    eb = T.element_size()
+    s = torch.cuda.current_stream()
+    inner = [([1, 1, 1], [n - 1, n - 1, n - 1])]
+    mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
+    bufs = [T, T2]
+
+    def plain(v, r):
+        k = [0]
+
+        def f():
+            src, dst = bufs[k[0] & 1], bufs[(k[0] + 1) & 1]
+            native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), [n, n, n], rd2, 1e-4, eb, inner, True,
+                               v, s.cuda_stream, r)
+            k[0] += 1
+        return f
+
+    def fused(fh, v, mode, r):
+        k = [0]
+
+        def f():
+            src, dst = bufs[k[0] & 1], bufs[(k[0] + 1) & 1]
+            fh.step(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), rd2, 1e-4, v, k[0], True, s.cuda_stream, r, mode)
+            k[0] += 1
+        return f
+
+    def bench(fns: dict) -> dict:
+        for f in fns.values():
+            for _ in range(2):
+                f()
+        times = {c: [] for c in fns}
+        for _ in range(a.rounds):
+            for c, f in fns.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(a.steps):
+                    f()
+                e1.record(s)
+                e1.synchronize()
+                times[c].append(e0.elapsed_time(e1) / a.steps)
+        return {c: sorted(t)[len(t) // 2] for c, t in times.items()}
+
+    compiled = set(v for v in range(len(native.diffusion3d_variants())) if native.diffusion3d_variant_compiled(v))
+    pl = bench({f"plain v{v}/r{r}": plain(v, r) for v in PLAIN if v in compiled for r in ROUNDS})
+    best_plain = min(pl, key=pl.get)
+    print(f"n={n}^3 {a.dtype}: best plain {best_plain} {pl[best_plain]:.4f} ms "
+          f"({3 * n ** 3 * eb / pl[best_plain] / 1e6:.0f} GB/s)", flush=True)
+    out = {"n": n, "dtype": a.dtype, "plain": pl, "best_plain": best_plain, "shapes": {}}
+    if a.candidates:
+        base = [tuple(int(x) for x in c.split("/")) for c in a.candidates.split(",")]
+    else:
+        base = list(FUSED)
+    for shape in a.shapes.split(","):
+        nb = neighbours(shape)
+        fh = native.FusedHalo(mesh, [n, n, n], eb, nb)
+        fh.set_fields(T.data_ptr(), T2.data_ptr())
+        cands = list(base)
+        if not a.candidates and any(nb[2][s_] >= 0 for s_ in range(2)):
+            cands += list(DIRECT) + (list(DIRECT_F32) if eb == 4 else [])
+        if not a.candidates:
+            cands += [(v, m | 8, r) for v, m, r in cands]
+        has_z = any(nb[2][s_] >= 0 for s_ in range(2))
+        # mode bit 2 compiles the z exchange out: only without a z neighbour
+        cands = [c for c in cands if native.diffusion3d_fused_variant_ok(c[0]) and not (has_z and c[1] & 2)]
+        fns = {f"v{v}/m{m}/r{r}": fused(fh, v, m, r) for v, m, r in cands}
+        fns["plain"] = plain(*[int(x[1:]) for x in best_plain.split()[1].split("/")])
+        t = bench(fns)
+        if a.inkernel > 0:  # the fastest forms again with the step sync inside the kernel
+            front = sorted((c for c in t if c != "plain"), key=t.get)[:a.inkernel]
+            fk = {}
+            for c in front:
+                v, m, r = (int(x[1:]) for x in c.split("/"))
+                fk[f"v{v}/m{m | 16}/r{r}"] = fused(fh, v, m | 16, r)
+            fk["plain"] = fns["plain"]
+            tk = bench(fk)
+            t["plain"] = min(t["plain"], tk.pop("plain"))
+            t.update(tk)
+        tp = t.pop("plain")
+        best = min(t, key=t.get)
+        ratio = t[best] / tp
+        out["shapes"][shape] = {"neighbours": nb, "plain_ms": tp, "fused_ms": t, "best": best, "ratio": ratio}
+        top = sorted(t.items(), key=lambda kv: kv[1])[:4]
+        print(f"{shape:5s} nb={nb}: plain {tp:.4f} | best fused {best} {t[best]:.4f} -> {ratio:.4f}x | "
+              + ", ".join(f"{k}={v:.4f}" for k, v in top[1:]), flush=True)
+        mesh.check_error()
+        del fh
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+    igg.finalize_global_grid()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -8,7 +8,10 @@
 #include <pybind11/stl.h>
 
 #include <chrono>
+#include <mutex>
 #include <thread>
+#include <utility>
+#include <vector>
 
 #include <hip/hip_runtime_api.h>
 
@@ -61,20 +64,50 @@ struct DlpackAlloc {
   int device;
 };
 
+// Freeing a field whose tensor was garbage-collected: kernels queued on any
+// stream may still use it, and a device synchronisation right here would
+// invalidate a hipGraph capture in progress on this thread. So the
+// release is DEFERRED: the buffer joins a list that is drained (one device
+// synchronisation, then hipFree) at the next native allocation, at
+// finalize_global_grid / model close, or at exit - never inside a capture.
+std::mutex g_deferred_mu;
+std::vector<std::pair<void*, int>> g_deferred;  // (pointer, device)
+
+void flush_deferred_frees() {
+  std::vector<std::pair<void*, int>> v;
+  {
+    std::lock_guard<std::mutex> lk(g_deferred_mu);
+    v.swap(g_deferred);
+  }
+  if (v.empty()) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  int synced = -1;
+  for (const auto& [p, dev] : v) {
+    if (dev != synced) {
+      (void)hipSetDevice(dev);
+      (void)hipDeviceSynchronize();  // no kernel may still use the buffers
+      synced = dev;
+    }
+    (void)hipFree(p);
+  }
+  (void)hipSetDevice(cur);
+}
+
 void dlpack_free(DLManagedTensor* t) {
   if (!t) return;
   auto* ctx = static_cast<DlpackAlloc*>(t->manager_ctx);
-  int cur = 0;
-  if (hipGetDevice(&cur) == hipSuccess && cur != ctx->device) (void)hipSetDevice(ctx->device);
-  (void)hipDeviceSynchronize();  // no kernel may still use the buffer
-  (void)hipFree(t->dl_tensor.data);
-  if (cur != ctx->device) (void)hipSetDevice(cur);
+  {
+    std::lock_guard<std::mutex> lk(g_deferred_mu);
+    g_deferred.emplace_back(t->dl_tensor.data, ctx->device);
+  }
   delete ctx;
   delete t;
 }
 
 py::capsule alloc_dlpack(size_t bytes, int kind) {
   if (bytes == 0) fail("alloc_dlpack: zero bytes");
+  flush_deferred_frees();  // allocation time is a safe point (no capture in progress)
   int dev = 0;
   IGG_HIP_CHECK(hipGetDevice(&dev));
   void* p = ipc_malloc(bytes, static_cast<MemKind>(kind));
@@ -262,6 +295,13 @@ PYBIND11_MODULE(_igg_native, m) {
     return reinterpret_cast<uintptr_t>(ipc_malloc(bytes, static_cast<MemKind>(kind)));
   });
   m.def("ipc_free", [](uintptr_t p) { ipc_free(reinterpret_cast<void*>(p)); });
+  m.def("flush_deferred_frees", &flush_deferred_frees,
+        "Free the native field buffers whose tensors were released (one device synchronisation); "
+        "called at finalize / model close. Never call it inside a hipGraph capture.");
+  m.def("deferred_frees", []() {
+    std::lock_guard<std::mutex> lk(g_deferred_mu);
+    return g_deferred.size();
+  });
   m.def("alloc_dlpack", &alloc_dlpack, py::arg("bytes"), py::arg("kind"),
         "Zeroed device allocation of a MemKind as a DLPack capsule (1-D uint8; torch.utils.dlpack.from_dlpack).");
   m.def("ipc_get_handle", [](uintptr_t p) { return py::bytes(ipc_get_handle(reinterpret_cast<void*>(p))); });
@@ -610,7 +650,7 @@ PYBIND11_MODULE(_igg_native, m) {
         py::arg("stream") = 0, py::arg("rounds") = 0);
   // Inner-box sweep through one restrict-form tiling id (fused_kernels.hip
   // dispatch_plain); the measurement-only tilings (incl. the timing probes
-  // 130-132 of benchmarks/refetch_probe.py) exist only in a --probes build.
+  // 130-132 of profiles/r2_refetch/refetch_probe.py) exist only in a --probes build.
   m.def("diffusion3d_hx_tiling",
         [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
            double dtlam, int elem_bytes, int tiling, uintptr_t stream, int rounds) {

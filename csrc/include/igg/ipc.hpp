@@ -28,7 +28,7 @@ enum class MemKind : int {
 // Largest allocation this framework exports through IPC. On this image
 // (ROCm 7.x, dmabuf IPC: HSA_ENABLE_IPC_MODE_LEGACY=0) hipIpcOpenMemHandle of
 // an allocation above 2 GiB never returns (2047 MiB opens in 0.4 ms, 2049 MiB
-// hangs: benchmarks/ipc_open_probe.py, profiles/r3_ipc/). ipc_get_handle
+// hangs: profiles/r3_ipc/ipc_open_probe.py, profiles/r3_ipc/). ipc_get_handle
 // refuses larger allocations with an error instead, so a collective caller
 // fails on every rank (or falls back) rather than hanging in the open.
 constexpr size_t IPC_MAX_BYTES = size_t{1} << 31;

@@ -9,6 +9,14 @@
 // every storing wave with s_waitcnt vmcnt(0) before the flag that publishes
 // the data is set (next kernel on the stream).
 //
+// INVARIANT for the in-kernel step synchronisation (send mode bit 16,
+// devsync.hpp step_sync_exit): the last exchanging wave publishes ARRIVED
+// with relaxed system-scope stores and NO release fence. That is correct only
+// because EVERY store a fused kernel makes into a peer's memory goes through
+// st_sys / st_sys_at (write-through, acknowledged before the wave counts
+// itself). A plain store into peer memory anywhere in a fused kernel would
+// break that form (docs/COHERENCE.md, "No release fence in K4").
+//
 // The stores are relaxed system-scope atomic stores of 1, 2, 4 or 8 bytes (a
 // wider value is split), which the compiler emits as `global_store_{byte,
 // short,dword,dwordx2} ... sc0 sc1` and schedules like any other memory instruction. (Rounds 2-3 used

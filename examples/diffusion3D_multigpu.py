@@ -3,8 +3,9 @@
 
 Counterpart of the reference's examples/diffusion3D_multigpu_CuArrays.jl: every
 ``--vis-every`` steps the halo-free interior of T is gathered on rank 0
-(gather_, device to device: RCCL receives + HIP reorder kernel on the root GPU)
-and a y-mid slice is appended to an animated GIF (utils/vis.py). Pass
+(gather_, device to device: on one node the root's copy engines pull every
+block over IPC straight into its place, parallel/gather.py; RCCL receives +
+HIP reorder kernel across nodes or with IGG_GATHER_PULL=0) and a y-mid slice is appended to an animated GIF (utils/vis.py). Pass
 ``--cpu`` for the multicpu variant (examples/diffusion3D_multicpu.jl).
 
     torchrun --standalone --local-addr 127.0.0.1 --nproc-per-node 8 \\

@@ -104,7 +104,7 @@ class Diffusion3D:
         self.T2 = self.T.clone()
         # One allocation with gaps between the three arrays: measured 1-3 %
         # faster than back-to-back 2 MiB-aligned tensors on MI355X
-        # (benchmarks/stencil_offsets.py: HBM channel placement).
+        # (profiles/r2_offsets/stencil_offsets.py: HBM channel placement).
         # field_memory (IGG_FIELD_MEMORY): "fine" (default: one native
         # fine-grained allocation) or "torch" (coarse-grained, torch's caching
         # allocator). The direct-z fused exchange stores into the neighbours'

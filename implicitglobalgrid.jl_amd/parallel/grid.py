@@ -285,5 +285,11 @@ def finalize_global_grid(*, finalize_MPI: bool = True) -> None:
             _comm.finalize_runtime()
     finally:
         set_global_grid(GLOBAL_GRID_NULL)
+        import gc
+
+        gc.collect()  # the reference runs GC.gc() here (finalize_global_grid.jl:26)
+        from .._native import native
+
+        native.flush_deferred_frees()  # native field buffers released by the collection
     if transport_error is not None:
         raise transport_error

@@ -7,7 +7,7 @@ hipMemcpyAsync D2D 4 MiB) and each placement (alone; concurrent on a
 high-priority stream; concurrent with CU-masked streams reserving R CUs) we
 time X with events on its own stream, plus the big kernel's duration.
 
-Usage: python benchmarks/concurrency_probe.py [--n 512] [--reps 5]
+Usage: python profiles/overlap/concurrency_probe.py [--n 512] [--reps 5]
 """
 import argparse
 import json
@@ -15,7 +15,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

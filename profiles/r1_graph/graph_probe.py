@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """Probe hipGraph capture/replay of a diffusion step, printing progress markers.
 
-Usage: python benchmarks/graph_probe.py {local|loopback} [--mode sequential|onephase] [--n 64]
+Usage: python profiles/r1_graph/graph_probe.py {local|loopback} [--mode sequential|onephase] [--n 64]
 """
 import argparse
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def mark(msg):

@@ -8,14 +8,14 @@ hipStreamWaitValue64 on the own flag, verification, and the ping-pong latency
 of CP flag signalling. Every wait is bounded on the host (stream query with a
 deadline; a stuck wait is released by writing the flag from another stream).
 
-Usage: python benchmarks/ipc_probe.py            (launches 2 ranks itself)
+Usage: python profiles/r1_put/ipc_probe.py            (launches 2 ranks itself)
 """
 import os
 import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -3,13 +3,13 @@
 dispatch_plain ids) on the model's own 512^3 f64 buffers, interleaved, median
 of repeats; each tiling's result is checked bitwise against tiling 11 first.
 
-Usage: python benchmarks/tiling_probe.py --tilings 11,124,140,141 [--rounds-grid 1,2,3]
+Usage: python profiles/r2_fullrow/tiling_probe.py --tilings 11,124,140,141 [--rounds-grid 1,2,3]
 """
 import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

@@ -4,7 +4,7 @@
 All three arrays are carved from one allocation with configurable byte gaps
 (channel/bank alignment study); variants are timed interleaved, median of rounds.
 
-Usage: python benchmarks/stencil_offsets.py [--n 512] [--variants 0,11] [--gaps 0,4096,65536,...]
+Usage: python profiles/r2_offsets/stencil_offsets.py [--n 512] [--variants 0,11] [--gaps 0,4096,65536,...]
 """
 import argparse
 import json
@@ -12,7 +12,7 @@ import os
 import statistics
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 
 import igg  # noqa: E402

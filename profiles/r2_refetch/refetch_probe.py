@@ -5,13 +5,13 @@ workgroup per CU) as is (124), without its z-segment edge loads (130), without
 its y-halo row loads (131), and without both (132). Ping-pong launches on two
 512^3 f64 buffers, interleaved, median of rounds.
 
-Usage: python benchmarks/refetch_probe.py [--n 512] [--rounds-grid 2,3]
+Usage: python profiles/r2_refetch/refetch_probe.py [--n 512] [--rounds-grid 2,3]
 """
 import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

@@ -7,13 +7,13 @@ vs forward/reversed pairs of the same tiling, on the model's own buffers
 (Diffusion3D placement), interleaved, median of repeats; plus a bitwise check of
 the reversed sweep against the forward one.
 
-Usage: python benchmarks/reverse_probe.py [--n 512] [--rounds-grid 2,3]
+Usage: python profiles/r2_reverse/reverse_probe.py [--n 512] [--rounds-grid 2,3]
 """
 import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import torch  # noqa: E402
 

@@ -10,7 +10,7 @@ prints how long export, open and first touch take for such sizes.
 Every step runs under the caller's `timeout`; a line is printed per step so a
 stuck step is named by the last line.
 
-Usage: python benchmarks/ipc_open_probe.py [--sizes-mib 64,1024,3300] [--kinds 0,1]
+Usage: python profiles/r3_ipc/ipc_open_probe.py [--sizes-mib 64,1024,3300] [--kinds 0,1]
        (launches 2 ranks itself; --share-gpu style: both on device 0 unless
        --per-rank-device)
 """
@@ -20,7 +20,7 @@ import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -151,19 +151,61 @@ def scenario_gather_fail(expect):
     os._exit(0)  # the failed gather's state is not torn down collectively
 
 
+def scenario_rccl_init_bounded(max_seconds):
+    """RCCL bootstrap bounded and collective: ranks sharing one GPU (RCCL
+    refuses duplicate devices) and/or a rank that arrives late
+    (IGG_INJECT_HANG=rccl_init@r:seconds) - every rank raises the same
+    IGGError within the bound, none hangs; a second attempt raises at once."""
+    import time as _time
+
+    _device("gpu")
+    me, dims, nprocs, coords, comm = igg.init_global_grid(6, 5, 4, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    t0 = _time.monotonic()
+    try:
+        comm.ensure_rccl()
+    except igg.IGGError as e:
+        dt = _time.monotonic() - t0
+        assert "RCCL communicator could not be created" in str(e), str(e)
+        assert dt < float(max_seconds), f"rank {me}: took {dt:.1f} s"
+        print(f"rank {me}: raised after {dt:.1f} s: {str(e)[:240]}", flush=True)
+    else:
+        raise AssertionError(f"rank {me}: RCCL with ranks sharing a GPU did not fail")
+    t1 = _time.monotonic()
+    try:
+        comm.ensure_rccl()
+    except igg.IGGError:
+        assert _time.monotonic() - t1 < 1.0, "a failed bootstrap was retried"
+    else:
+        raise AssertionError("second ensure_rccl did not raise")
+    igg.finalize_global_grid()
+    print(f"rank {me} rccl init bounded OK", flush=True)
+
+
 def scenario_diffusion(dev, nx, ny, nz, steps, overlap):
     from igg.models.diffusion3d import Diffusion3D
     from igg.ops import stencil
 
     device = _device(dev)
     nx, ny, nz, steps = int(nx), int(ny), int(nz), int(steps)
-    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, quiet=True, select_device=False,
+    # IGG_TEST_DIMS="a,b,c" fixes the topology (e.g. 2,2,1: two split dims);
+    # IGG_TEST_GRAPH=k captures k steps in a hipGraph and replays them
+    dims_env = [int(v) for v in os.environ.get("IGG_TEST_DIMS", "0,0,0").split(",")]
+    me, dims, nprocs, coords, comm = igg.init_global_grid(nx, ny, nz, dimx=dims_env[0], dimy=dims_env[1],
+                                                          dimz=dims_env[2], quiet=True, select_device=False,
                                                           device_type="none" if dev == "cpu" else "AMDGPU")
     gg = igg.get_global_grid()
     v = os.environ.get("IGG_TEST_VARIANT")
     m = Diffusion3D(dtype=torch.float64, device=device, overlap=bool(int(overlap)),
                     variant=None if v is None else int(v))
-    m.run(steps)
+    g = int(os.environ.get("IGG_TEST_GRAPH", "0"))
+    if g:
+        assert m.overlap == bool(int(overlap))
+        m.capture(steps=g)  # performs the eager first step itself (no step is run by the capture)
+        m.run(steps - 1)  # graph replays (after at most two eager steps that realign the buffers)
+        assert steps - 1 >= g + 2, "too few steps for a replay"
+    else:
+        m.run(steps)
     loc = m.T.cpu()
     # global reference: same physics on the implicit global grid, one array
     ng = [int(v) for v in gg.nxyz_g]

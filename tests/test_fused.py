@@ -284,10 +284,11 @@ def test_graph_after_odd_step_counts(gpu):
 def test_in_kernel_step_sync_counts_every_step(gpu, variant, mode, periods):
     """The in-kernel step synchronisation advances EPOCH exactly once per step
     and leaves COUNT at 0: the host's count of exchanging waves equals the
-    number of waves that count themselves (a mismatch would stall a real
-    neighbour). Eager steps and graph replays."""
-    a, b = _pair((26, 37, 136), periods, torch.float64, variant, mode=mode)
-    assert b._fh.in_kernel_sync
+    neighbour). Eager steps and graph replays. The in-kernel form is send mode
+    bit 16 (the default is the sync kernel after the stencil)."""
+    a, b = _pair((26, 37, 136), periods, torch.float64, variant, mode=mode | 16)
+    assert not b._fh.in_kernel_sync  # default send modes: the sync kernel
+    assert b._fh.in_kernel_sync_for(b.fused_mode)
     e0 = b._fh.flag(0)
     b.run(3)
     torch.cuda.synchronize()

@@ -123,6 +123,32 @@ def test_diffusion_gpu_multirank_put(overlap):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("queues", ["1", "4"])
+def test_diffusion_overlap_graph_two_split_dims(queues):
+    """The boundary/interior overlapped step captured in a hipGraph and
+    replayed on a 2x2x1 decomposition (the N = 4 shape of a node): round 3's
+    SIGSEGV in the replay (profiles/r3_overlap_crash/, root cause in
+    profiles/r4_overlap_crash/: one hardware queue per process). Checked
+    against the global single-array solution."""
+    run_ranks(4, "diffusion", "gpu", 24, 20, 18, 7, 1,
+              env_extra={**PUT_ENV, "IGG_TEST_DIMS": "2,2,1", "IGG_TEST_GRAPH": "4", "GPU_MAX_HW_QUEUES": queues},
+              timeout=160)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("late", [False, True])
+def test_rccl_bootstrap_is_bounded_and_collective(late):
+    """Two ranks on one GPU: RCCL refuses the duplicate device (an asynchronous
+    error of the non-blocking bootstrap); with rank 1 arriving 25 s late, rank
+    0's bootstrap times out after IGG_FIRST_CONTACT_TIMEOUT = 8 s and is
+    aborted. Either way every rank raises the same error, none hangs."""
+    env = {"IGG_FIRST_CONTACT_TIMEOUT": "8"}
+    if late:
+        env["IGG_INJECT_HANG"] = "rccl_init@1:25"
+    run_ranks(2, "rccl_init_bounded", 60 if late else 30, env_extra=env, timeout=120)
+
+
+@pytest.mark.gpu
 def test_put_transport_timeout_reports_and_never_hangs():
     run_ranks(2, "put_timeout", env_extra={**PUT_ENV, "IGG_PUT_TIMEOUT": "2"}, timeout=120)
 
