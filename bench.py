@@ -106,7 +106,8 @@ def parse():
     ap.add_argument("--dtype", default=None, choices=["float64", "float32"])
     ap.add_argument("--gather-every", type=int, default=None, help="gather_ the field to rank 0 every K steps")
     ap.add_argument("--gather-mode", default="async", choices=["async", "sync"],
-                    help="async: snapshot + gather_async_ (root pulls with copy engines while stepping continues)")
+                    help="async: gather_async_(snapshot=True): one copy per rank, then the root pulls with its "
+                         "copy engines while stepping continues")
     ap.add_argument("--overlap", action="store_true",
                     help="force the boundary/interior split with the halo on a second stream (default: A/B decides)")
     ap.add_argument("--variant", default=None, help="stencil kernel variant (int) or 'auto'")
@@ -978,7 +979,7 @@ def main():
         t0 = time.perf_counter()
         if gather_every > 0:
             done, pending = 0, None
-            snap = torch.empty_like(field()) if args.gather_mode == "async" and on_gpu else None
+            async_gather = args.gather_mode == "async" and on_gpu
             while done < args.steps:
                 k = min(gather_every, args.steps - done)
                 model.run(k)
@@ -986,13 +987,15 @@ def main():
                 if done % gather_every == 0:
                     if getattr(model, "fused", False):
                         model.sync_halo()  # fused steps leave the halo planes stale
-                    if snap is None:
+                    if not async_gather:
                         igg.gather_(field(), A_global)
                     else:
                         if pending is not None:
                             pending.wait()
-                        snap.copy_(field())
-                        pending = igg.gather_async_(snap, A_global)
+                        # snapshot: every rank copies T now (its staging chunks /
+                        # the root's block of A_global), the only serial part; the
+                        # root pulls the chunks while the next steps run
+                        pending = igg.gather_async_(field(), A_global, snapshot=True)
             if pending is not None:
                 pending.wait()
         else:

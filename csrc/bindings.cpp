@@ -558,8 +558,11 @@ PYBIND11_MODULE(_igg_native, m) {
            }),
            py::arg("rank"), py::arg("nranks"), py::arg("allgather"))
       .def("start", [](PullGatherer& g, const FieldTuple& a, uintptr_t dst, int root, const Int3& dims,
-                       uintptr_t s) { g.start(to_field(a), reinterpret_cast<void*>(dst), root, dims, as_stream(s)); },
-           py::arg("a"), py::arg("dst"), py::arg("root"), py::arg("dims"), py::arg("stream"))
+                       uintptr_t s, bool snapshot) {
+             g.start(to_field(a), reinterpret_cast<void*>(dst), root, dims, as_stream(s), snapshot);
+           },
+           py::arg("a"), py::arg("dst"), py::arg("root"), py::arg("dims"), py::arg("stream"),
+           py::arg("snapshot") = false)
       .def("wait", [](PullGatherer& g, uintptr_t s) { g.wait(as_stream(s)); }, py::arg("stream"))
       .def_property_readonly("pending", &PullGatherer::pending)
       .def("free", &PullGatherer::free);

@@ -150,7 +150,8 @@ void PullGatherer::free() {
   stage_bytes_ = 0;
 }
 
-void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream) {
+void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream,
+                         bool snapshot) {
   TraceRange tr("igg.gather_async.start");
   if (pending_) fail("gather_async: a gather is already pending (call wait() first)");
   if (!a.device) fail("gather_async: the local array must be a GPU array.");
@@ -174,7 +175,9 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
       IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(a.ptr)));
       bool forced = false;
       const size_t cap = chunk_cap(&forced);
-      if (size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
+      // snapshot: `a` may change as soon as start() returns, so it is copied
+      // into the staging chunks in any case (the chunks are the snapshot).
+      if (snapshot || size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
         // Stage into exportable chunks of whole planes (class comment).
         const int64_t ppc = std::max<int64_t>(1, static_cast<int64_t>(cap / std::max<size_t>(plane, 1)));
         const size_t cb = static_cast<size_t>(ppc) * plane;
@@ -302,7 +305,9 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
           std::memcpy(&off, rec.data() + hdr + MH, 8);
           src = static_cast<const char*>(per[0].second) + off;
         }
-        copy_block(src, dst, a.size, dims, c, 0, a.size[0], a.elem_bytes, s);
+        // the root's own block under snapshot: copied on the caller's stream
+        // now, so `a` may change right after start() like on the other ranks
+        copy_block(src, dst, a.size, dims, c, 0, a.size[0], a.elem_bytes, (snapshot && p == root) ? stream : s);
       }
       for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipEventRecord(done_[k], side_[k]));
     } else {

@@ -81,7 +81,12 @@ class PullGatherer {
   PullGatherer& operator=(const PullGatherer&) = delete;
   // `dst` (root only): C-contiguous device array of extent dims*size; `stream`:
   // the stream on which `a` is produced (and, on the root, dst is consumed).
-  void start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream);
+  // `snapshot`: every rank copies `a` now, on `stream` (non-root ranks into
+  // their exportable staging chunks, the root straight into its place in
+  // dst), so `a` may be modified as soon as start() returns - the copy is the
+  // only serial part of the gather; the pulls of the chunks overlap whatever
+  // the ranks do next.
+  void start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream, bool snapshot = false);
   void wait(hipStream_t stream);
   bool pending() const { return pending_; }
   void free();

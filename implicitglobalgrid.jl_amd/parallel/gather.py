@@ -183,7 +183,8 @@ class GatherHandle:
         return self._done
 
 
-def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) -> GatherHandle:
+def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0,
+                  snapshot: bool = False) -> GatherHandle:
     """Non-blocking ``gather_``: returns a handle whose ``wait()`` (collective)
     completes it. GPU fields on several ranks: the root pulls every block with
     the copy engines straight into its place in ``A_global`` (one 3-D
@@ -192,7 +193,13 @@ def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int =
     drain at the call, no compute units, no staging buffer) while the
     application continues; ``A`` must not be modified before ``wait()``
     (MPI_Igather semantics) and ``A_global`` (root) must be a C-contiguous GPU
-    tensor. Other cases complete synchronously."""
+    tensor. Other cases complete synchronously.
+
+    ``snapshot=True``: every rank copies ``A`` at the call, stream-ordered
+    (into its exportable staging chunks; the root straight into its block of
+    ``A_global``), and ``A`` may be modified right away: the copy is the only
+    serial part; the root's pulls of the chunks overlap the ranks' next steps
+    (in-situ visualisation every K steps, BASELINE config 5)."""
     global _puller
     gg = _grid.global_grid()
     nprocs, me = int(gg.nprocs), int(gg.me)
@@ -212,13 +219,13 @@ def gather_async_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int =
             raise IGGError("gather_async_: A_global must be a C-contiguous GPU tensor on the root.")
         _global_view(A_global, _padded_shape(A), [int(d) for d in gg.dims])
     if not A.is_contiguous():
-        raise IGGError("gather_async_: A must be contiguous (it is read in place by the root).")
+        raise IGGError("gather_async_: A must be contiguous (it is read in place by the root, or snapshot).")
     if _puller is None:
         c = gg.comm
         _puller = native.PullGatherer(me, nprocs, lambda b: c.all_gather_object(bytes(b)))
     dims = [int(d) for d in gg.dims]
     _puller.start(field_tuple(A), A_global.data_ptr() if me == root else 0, root, dims,
-                  torch.cuda.current_stream().cuda_stream)
+                  torch.cuda.current_stream().cuda_stream, bool(snapshot))
     return GatherHandle(A_global if me == root else None, False)
 
 

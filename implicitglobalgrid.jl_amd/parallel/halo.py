@@ -166,8 +166,30 @@ def _init_engine(gg) -> None:
     _set_poll_every(config.poll_every())
     if gg.nprocs > 1:
         _engine.set_transport(gg.comm.host_transport(), False)
-        if gg.amdgpu_enabled:
-            _engine.set_transport(gg.comm.device_transport(), True)
+        # The device transport (RCCL communicator, put mesh) is created by the
+        # first device exchange, not here: init_global_grid must not depend on
+        # a first contact with the other GPUs (a bootstrap that fails or hangs
+        # fails that exchange - or the transport validation that selects
+        # another transport - not the grid itself).
+        _set_dev_pending(bool(gg.amdgpu_enabled))
+
+
+_dev_pending = False
+_PENDING_NAMES = {"rccl": "rccl", "put": "put", "staged": "gloo-staged", "torch": "torch-nccl"}
+
+
+def _set_dev_pending(flag: bool) -> None:
+    global _dev_pending
+    _dev_pending = flag
+
+
+def _ensure_device_transport() -> None:
+    """Create the configured device transport on first use (collective: every
+    rank's first device exchange happens at the same point)."""
+    global _dev_pending
+    if _dev_pending:
+        _dev_pending = False
+        _engine.set_transport(_grid.global_grid().comm.device_transport(), True)
 
 
 _poll_every = 1000
@@ -187,6 +209,7 @@ def _drop_engine() -> None:
         _engine.pool_free()
     _engine = None
     _loopback_comm = None
+    _set_dev_pending(False)
 
 
 def set_transport(name: str) -> None:
@@ -199,6 +222,7 @@ def set_transport(name: str) -> None:
     if not gg.amdgpu_enabled:
         raise IGGError("set_transport: the grid was not initialised for GPU fields")
     _engine.set_transport(gg.comm.device_transport(name), True)
+    _set_dev_pending(False)
     _sig_modes.clear()
     for p in _plans.values():
         p[3] = None  # schedule costs differ per transport: 'auto' measures again
@@ -207,6 +231,8 @@ def set_transport(name: str) -> None:
 def transport_name() -> str:
     """Name of the device transport update_halo_ currently uses ('none' if single-process)."""
     _grid.check_initialized()
+    if _dev_pending:  # not created yet: the configured choice
+        return _PENDING_NAMES[config.transport_choice()]
     return _engine.transport_name(True)
 
 
@@ -440,6 +466,8 @@ def update_halo_(*fields) -> None:
         return
     p = _plan(fields)
     fs, device, dtype, mode = p
+    if device and _dev_pending:
+        _ensure_device_transport()
     stream = torch.cuda.current_stream().cuda_stream if device else 0
     if mode is None and device and _engine.mode == HALO_MODES["auto"]:
         sig = tuple((tuple(A.shape), tuple(A.stride()), A.dtype) for A in fields)

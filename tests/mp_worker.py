@@ -537,6 +537,27 @@ def scenario_gather_async():
                     exp = (torch.full(s, float(p + 1), dtype=torch.float64) * 1000
                            + torch.arange(120, dtype=torch.float64).view(s)).to(dt).double()
                     assert torch.equal(blk, exp), f"root {root}: block of rank {p} wrong"
+            # snapshot=True: A may change right after the call (the copy is
+            # stream-ordered before the change), the gather still sees the
+            # values of the call
+            A.copy_(final)
+            if me == root:
+                G.zero_()
+            h = igg.gather_async_(A, G, root=root, snapshot=True)
+            A.fill_(-5)  # before wait(): allowed with snapshot
+            delay = torch.rand(1024, 1024, device="cuda", dtype=torch.float64)
+            delay = delay @ delay
+            h.wait()
+            torch.cuda.synchronize()
+            del delay
+            if me == root:
+                Gc = G.cpu().double()
+                for p in range(nprocs):
+                    c = igg.native.cart_coords(p, dims.tolist())
+                    blk = Gc[c[0] * 6:(c[0] + 1) * 6, c[1] * 5:(c[1] + 1) * 5, c[2] * 4:(c[2] + 1) * 4]
+                    exp = (torch.full(s, float(p + 1), dtype=torch.float64) * 1000
+                           + torch.arange(120, dtype=torch.float64).view(s)).to(dt).double()
+                    assert torch.equal(blk, exp), f"snapshot, root {root}: block of rank {p} wrong"
     igg.finalize_global_grid()
     print(f"rank {me} gather_async OK")
 

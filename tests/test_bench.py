@@ -52,6 +52,26 @@ def test_post_validation_fails_closed():
     assert "post-timing validation failed" in r.stderr
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_stencil_post_check_fails_closed(n):
+    """After the timed region the same K steps are recomputed from the saved
+    starting state (on a GPU through a second compiled stencil variant) and
+    compared bitwise: a mismatch (injected on rank 0) means no result line,
+    at N = 1 too."""
+    r, rec = _run(["--gpus", str(n), "--device", "cpu", "--n", "20", "--steps", "3", "--warmup", "1"],
+                  IGG_BENCH_INJECT="stencil_post")
+    assert r.returncode != 0
+    assert rec is None
+    assert "post-timing stencil check failed" in r.stderr
+
+
+def test_stencil_post_check_recorded_at_n1():
+    r, rec = _run(["--gpus", "1", "--device", "cpu", "--n", "20", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    sp = rec["config"]["stencil_post_check"]
+    assert sp["result"] == "ok" and sp["steps"] == 3
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_self_launch_reports_n_gpus(n):
     r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--device", "cpu", "--n", "24", "--steps", "4",
