@@ -309,6 +309,8 @@ def _path_key(model) -> str | None:
 
     if getattr(model, "fused", False):
         return "fused-inkernel" if getattr(model, "fused_mode", 0) & 16 else "fused"
+    if getattr(model, "overlap", False):
+        return "overlap"
     return _transport_key(H.transport_name())
 
 
@@ -485,13 +487,15 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
     # rows, z-planes of a C-ordered field are maximally strided. (RCCL's p2p
     # kernels next to a full-GPU stencil measured slower than serial in
     # loopback, profiles/r1_ctas/; over real xGMI the A/B decides.)
-    # Not by default: replaying the captured overlapped put step crashed
-    # (SIGSEGV inside hipGraph replay, every rank) with x AND y neighbours
-    # (4 ranks, 2x2x1, 512^3; 2x1x1 replays fine): profiles/r3_overlap_crash/.
-    # A crash cannot be caught, and the fused exchange is the hiding mechanism
-    # the A/B keeps anyway; IGG_BENCH_OVERLAP=1 puts them back.
-    if (os.environ.get("IGG_BENCH_OVERLAP") == "1" and getattr(model, "can_overlap", False)
-            and not any(model.sides[2])):
+    # Round 3 took them out of the default A/B after a SIGSEGV in the replay of
+    # the captured overlapped put step (4 ranks sharing a GPU, 2x2x1,
+    # profiles/r3_overlap_crash/); round 4 traced it to processes with ONE
+    # hardware queue (GPU_MAX_HW_QUEUES=1, which the shared-GPU rehearsal
+    # sets), where the model now runs the three parts in stream order
+    # (profiles/r4_overlap_crash/). A crash of a candidate is a supervisor
+    # relaunch without 'overlap'. IGG_BENCH_OVERLAP=0 leaves them out.
+    if (os.environ.get("IGG_BENCH_OVERLAP", "1") != "0" and "overlap" not in EXCL
+            and getattr(model, "can_overlap", False) and not any(model.sides[2])):
         if valid.get("put") == "ok":
             cands.append(("put+overlap", "put", "auto", True))
         if valid.get("rccl-sequential") == "ok":
@@ -503,7 +507,7 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
         raise RuntimeError("no device transport passed the bitwise validation against the host-staged path")
     times = {}
     for name, t, mode, ov in cands:
-        PH.enter(f"ab:{name}", _transport_key(t), deadline=300)
+        PH.enter(f"ab:{name}", "overlap" if ov else _transport_key(t), deadline=300)
         H.set_transport(t)
         H.set_halo_mode(mode)
         if hasattr(model, "set_overlap"):

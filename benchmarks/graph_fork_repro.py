@@ -36,6 +36,9 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--replays", type=int, default=50)
     ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--branches", type=int, default=1,
+                    help="side streams forked per step (concurrent graph branches besides the capture stream)")
+    ap.add_argument("--kernels", type=int, default=1, help="kernels per branch per step")
     args = ap.parse_args()
     faulthandler.enable()
     import torch
@@ -45,23 +48,31 @@ def main() -> int:
 
         native.install_crash_handler()
     a = torch.zeros(args.n, device="cuda")
-    b = torch.zeros(args.n, device="cuda")
-    side = None
+    bs = [torch.zeros(args.n, device="cuda") for _ in range(max(1, args.branches))]
+    sides = []
     if args.side != "none":
         lo, hi = torch.cuda.Stream.priority_range()
         prio = {"default": 0, "high": hi, "low": lo}[args.side]
-        side = torch.cuda.Stream(priority=prio)
+        sides = [torch.cuda.Stream(priority=prio) for _ in range(args.branches)]
     main_s = torch.cuda.Stream()
 
     def step():
-        a.add_(1.0)
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                b.add_(1.0)
-            torch.cuda.current_stream().wait_stream(side)
+        for _ in range(args.kernels):
+            a.add_(1.0)
+        if sides:
+            cur = torch.cuda.current_stream()
+            for sd in sides:
+                sd.wait_stream(cur)
+            for sd, b in zip(sides, bs):
+                with torch.cuda.stream(sd):
+                    for _ in range(args.kernels):
+                        b.add_(1.0)
+            for sd in sides:
+                cur.wait_stream(sd)
         else:
-            b.add_(1.0)
+            for b in bs:
+                for _ in range(args.kernels):
+                    b.add_(1.0)
 
     with torch.cuda.stream(main_s):
         step()  # warm-up (allocator, kernels)
@@ -72,14 +83,16 @@ def main() -> int:
             for _ in range(args.steps):
                 step()
     torch.cuda.synchronize()
-    print(f"captured {args.steps} steps (side stream: {args.side}, GPU_MAX_HW_QUEUES="
+    print(f"captured {args.steps} steps ({args.branches} side stream(s): {args.side}, {args.kernels} kernel(s) "
+          f"per branch, GPU_MAX_HW_QUEUES="
           f"{os.environ.get('GPU_MAX_HW_QUEUES')}); replaying {args.replays} times", flush=True)
     for _ in range(args.replays):
         g.replay()
     torch.cuda.synchronize()
-    want = 1 + args.steps * args.replays
-    ok = bool((a == want).all().item() and (b == want).all().item())
-    print(f"replays done: a={a[0].item():.0f} b={b[0].item():.0f} (want {want}): {'OK' if ok else 'WRONG'}", flush=True)
+    want = args.kernels * (1 + args.steps * args.replays)
+    ok = bool((a == want).all().item() and all((b == want).all().item() for b in bs))
+    print(f"replays done: a={a[0].item():.0f} b0={bs[0][0].item():.0f} (want {want}): {'OK' if ok else 'WRONG'}",
+          flush=True)
     return 0 if ok else 1
 
 

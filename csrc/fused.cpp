@@ -119,7 +119,7 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
     x.sync = step_sync_from(sync_);
     x.sync_used = &used;
   }
-  launch_diffusion3d_fused(a, x, variant, mode & 15, stream);
+  launch_diffusion3d_fused(a, x, variant, mode & ~IN_KERNEL_SYNC, stream);
   if (!used) sync(stream);
   open_ = used;
 }

@@ -86,8 +86,53 @@ struct HxScal {
   int64_t* stamps;
   int force_sel;
   int peel;  // send mode bit 8: sweep the exchanged x planes of a chunk separately (kernel below)
+  // Send mode bit 32: dispatch the exchanging z-edge tiles first (hx_tile).
+  // order_lo: z tile 0 exchanges; order_hi: the z tile holding n2-VZ (index
+  // tz_hi) exchanges.
+  int order, order_lo, order_hi;
+  int64_t tz_hi;
   StepSync sync;  // in-kernel step synchronisation (put.hpp; my_flags null: a sync kernel follows)
 };
+
+// Tile (z tile, y tile, x chunk) of block `bid` of `nblk`. Default: z tiles
+// fastest, so the z tiles of one row-chunk are neighbours in dispatch order
+// and (xcd_remap) on one XCD's L2; the x chunks holding the exchanged planes
+// come first (hx_chunk). With a.order (send mode bit 32) the z-EDGE tiles of an
+// exchanging z side are dispatched first - longest work first. The z-edge
+// waves carry the z sends (+8-11 % per wave, profiles/r3_waves/); with the
+// default order they are spread evenly over the launch, so at 2 residency
+// rounds every other slot runs one heavy and one light wave and the kernel
+// takes (1 + 0.106)/1 of the plain time however few of them there are (a
+// 2x2x2 corner rank: a quarter). Dispatched first, they run in the first
+// round(s) while later rounds' light waves fill the slots they leave: with
+// enough rounds the kernel approaches the average instead of the maximum.
+// Scheduling only: the results are unchanged.
+template <typename T>
+struct HxTile {
+  int64_t tz, ty, cx;
+};
+
+template <typename T>
+__device__ __forceinline__ HxTile<T> hx_tile(const HxScal<T>& a, int64_t bid, int64_t nblk) {
+  const int64_t nch = (a.n0 - 2 + a.ch - 1) / a.ch;
+  if (a.order && (a.order_lo || a.order_hi)) {
+    const int64_t R = a.nty * nch;  // row-chunks per z tile
+    const int64_t tzi = bid / R;
+    const int64_t rc = xcd_remap(bid - tzi * R, R);
+    const int nh = (a.order_lo ? 1 : 0) + ((a.order_hi && !(a.order_lo && a.tz_hi == 0)) ? 1 : 0);
+    int64_t tz;
+    if (tzi < nh) {
+      tz = (tzi == 0 && a.order_lo) ? 0 : a.tz_hi;
+    } else {
+      tz = tzi - nh + (a.order_lo ? 1 : 0);  // the light tiles in ascending order
+      if (a.order_hi && a.tz_hi != 0 && tz >= a.tz_hi) ++tz;
+    }
+    return {tz, rc % a.nty, hx_chunk(rc / a.nty, nch)};
+  }
+  const int64_t b = xcd_remap(bid, nblk);
+  const int64_t rest = b / a.ntz;
+  return {b % a.ntz, rest % a.nty, hx_chunk(rest / a.nty, nch)};
+}
 
 // Writer side of the cross-device hand-off: every store into peer memory
 // (arena regions, or the neighbour's field with direct z) is a system-scope
@@ -125,17 +170,19 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   constexpr bool RV = (FEAT & 65536) != 0;
   static_assert(!RV || (FEAT & (1 | 2 | 4 | 8 | 64 | 128 | 4096 | 8192)) == 0, "RV: plain sweeps only");
   constexpr int64_t DX = RV ? -1 : 1;
-  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t tz = b % a.ntz;
-  const int64_t rest = b / a.ntz;
-  const int64_t ty = rest % a.nty;
   // Chunks holding the x send planes run first (order 0, last, 1, 2, ...): the
   // plane x=n0-2 is computed in the last step of the last chunk, so with >= 2
   // residency rounds its remote stores drain while later rounds compute
   // instead of at the kernel's tail. Scheduling only: results are unchanged.
+  // (hx_tile; send mode bit 32 also puts the z-edge tiles first.)
   const int64_t nch = (a.n0 - 2 + a.ch - 1) / a.ch;
-  const int64_t cxr = rest / a.nty;
-  const int64_t cx = RV ? nch - 1 - cxr : hx_chunk(cxr, nch);
+  const HxTile<T> tile = hx_tile(a, blockIdx.x, gridDim.x);
+  const int64_t tz = tile.tz, ty = tile.ty;
+  int64_t cx = tile.cx;
+  if constexpr (RV) {  // reversed march (probe form): chunks from the top, default order
+    const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+    cx = nch - 1 - (b / a.ntz) / a.nty;
+  }
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wz = wid % BZ, wy = wid / BZ;
@@ -512,12 +559,9 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     IGG_HX_SWEEP(FEAT);  // nothing to specialise, or specialisation disabled (FEAT 2048)
   } else {
     constexpr int W = 64 * VZ * BZ;
-    const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
-    const int64_t rest = b / a.ntz;
-    const int64_t tz = b % a.ntz, ty = rest % a.nty;
+    const HxTile<T> tile = hx_tile(a, blockIdx.x, gridDim.x);
+    const int64_t tz = tile.tz, ty = tile.ty, cx = tile.cx;
     const int64_t n0 = a.n0, n1 = a.n1, n2 = a.n2;
-    const int64_t nch = (n0 - 2 + a.ch - 1) / a.ch;
-    const int64_t cx = hx_chunk(rest / a.nty, nch);
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wz = wid % BZ, wy = wid / BZ;
     const int64_t zt = tz * W + wz * (64 * VZ);
@@ -631,7 +675,8 @@ int64_t hx_feature_waves(int64_t n0, int64_t n1, int64_t n2, int64_t ch, int64_t
 }
 
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
-void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream, bool peel = false) {
+void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream, bool peel = false,
+               bool order = false) {
   const int64_t n0 = d.n[0], n1 = d.n[1], n2 = d.n[2];
   if (n2 % VZ != 0 || n2 < 2 * VZ)
     fail("diffusion3d (fused halo): n2 must be a multiple of ", VZ, " and >= ", 2 * VZ);
@@ -660,6 +705,11 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   a.stamps = g_hx_stamps;
   a.force_sel = g_hx_force_sel;
   a.peel = peel ? 1 : 0;
+  constexpr int FZ_ = FEAT & (4 | 8);
+  a.order = order ? 1 : 0;
+  a.order_lo = (FZ_ != 0 && (io.in[2][0] || io.out[2][0])) ? 1 : 0;
+  a.order_hi = (FZ_ != 0 && (io.in[2][1] || io.out[2][1])) ? 1 : 0;
+  a.tz_hi = (n2 - VZ) / W;
   a.sync = StepSync{};
   // In-kernel step sync: the specialised kernel only (per-wave feature
   // classes), and not under the diagnostics that override the classes.
@@ -699,6 +749,10 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
 // arena region, so no wave patches a received z halo into its rows (the cost
 // of the z-edge waves of tilings 11/40: profiles/r2_fused_spec/).
 //
+// Mode bit 32 (order): the z-edge tiles of an exchanging z side are dispatched
+// first (hx_tile: longest work first), so with several residency rounds their
+// extra time is spread over the slots instead of setting the tail.
+//
 // Mode bit 8 (peel): a wave of an x-exchange chunk sweeps x = 1 and x = n0-2
 // with the x features and the planes in between without them (the x code in
 // the loop slows the whole chunk's march: profiles/r2_f32_fused/ class 1).
@@ -714,22 +768,23 @@ void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStre
   }
   const bool zx = io.in[2][0] || io.in[2][1] || io.out[2][0] || io.out[2][1];
   const bool pk = (mode & 8) != 0;  // peel the exchanged x planes (kernel)
+  const bool ord = (mode & 32) != 0;  // z-edge tiles first (hx_tile)
   mode &= 7;
   if ((mode & 4) && zx) {
     // Direct z (FEAT 203 = 207 without z-in): the z sends land in the
     // receivers' field halo elements, so the z-edge waves read their halo
     // from the field like every other wave and carry only the send code.
     if (io.in[2][0] || io.in[2][1]) fail("diffusion3d (fused halo): direct z mode with z arena input");
-    if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF>(d, io, s, pk);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF>(d, io, s, pk);
+    if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF>(d, io, s, pk, ord);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF>(d, io, s, pk, ord);
   } else if (zx || !(mode & 2)) {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s, pk);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s, pk);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s, pk, ord);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s, pk, ord);
   } else {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF>(d, io, s, pk);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF>(d, io, s, pk);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF>(d, io, s, pk, ord);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF>(d, io, s, pk, ord);
   }
 }
 

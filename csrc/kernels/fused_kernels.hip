@@ -90,7 +90,8 @@ bool diffusion3d_fused_variant_ok(int v) {
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
                               hipStream_t stream) {
   if (a.n[0] < 3 || a.n[1] < 3 || a.n[2] < 3) fail("diffusion3d: every extent must be >= 3");
-  if (mode < 0 || mode > 15) fail("diffusion3d (fused halo): mode must be 0..15");
+  if (mode < 0 || mode > 63 || (mode & 16))
+    fail("diffusion3d (fused halo): send mode must be 0..63 without bit 16 (step sync: FusedHalo)");
   if (a.elem_bytes != 8 && a.elem_bytes != 4) fail("diffusion3d: only float32/float64 are supported");
   if (!fused_launch_t0(a, io, variant, mode, stream) && !fused_launch_t11(a, io, variant, mode, stream) &&
       !fused_launch_misc(a, io, variant, mode, stream))

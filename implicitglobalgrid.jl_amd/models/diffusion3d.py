@@ -331,6 +331,15 @@ class Diffusion3D:
             self._fentry = False
             self._fstep += 1
             self._fprimed = True
+        elif self.overlap and _single_hw_queue():
+            # One hardware queue per process (GPU_MAX_HW_QUEUES=1, e.g. many
+            # ranks sharing a GPU): streams cannot run concurrently, and a
+            # hipGraph captured with the forked exchange crashed in replay
+            # (profiles/r4_overlap_crash/). Same three parts in stream order -
+            # identical results (disjoint writes), nothing lost.
+            stencil.diffusion3d_(T2, T, Cp, boxes=self.slabs, **self._kw(self.halo_variant, self.halo_rounds))
+            update_halo_(T2)
+            stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw(None, self.interior_rounds))
         elif self.overlap:
             # 1. boundary slabs on the compute stream (full bandwidth, nothing
             #    else running), 2. the halo exchange of T2 on the high-priority
@@ -450,6 +459,14 @@ class Diffusion3D:
     def a_eff_bytes(self) -> int:
         """A_eff = (2*D_u + D_k) * n_local * sizeof(T) with D_u = D_k = 1."""
         return 3 * self.T.numel() * self.T.element_size()
+
+
+def _single_hw_queue() -> bool:
+    """The HIP runtime of this process uses one hardware queue
+    (GPU_MAX_HW_QUEUES=1): its streams serialise."""
+    import os
+
+    return os.environ.get("GPU_MAX_HW_QUEUES", "").strip() == "1"
 
 
 def _make_fused_halo(m: "Diffusion3D"):

@@ -121,7 +121,7 @@ def test_fused_direct_z_matches_update_halo(gpu, variant, dtype, mode, periods):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [8, 9, 12, 13])
+@pytest.mark.parametrize("mode", [8, 9, 12, 13, 40, 44, 45])  # + 32: z-edge tiles dispatched first
 @pytest.mark.parametrize("variant", [0, 14, 40, 42, 44])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("periods", [(1, 1, 1), (1, 0, 1)])

@@ -214,7 +214,9 @@ def test_gather_pull_failure_is_collective_gpu(inject, expect):
                                                (8, (16, 18, 24, 6, 1, 1), ("0", "5")),
                                                # peeled x planes (mode bit 8) with remote x neighbours
                                                (2, (40, 66, 136, 6, 1, 0), ("42", "12")),
-                                               (8, (34, 66, 136, 5, 1, 1), ("40", "8"))])
+                                               (8, (34, 66, 136, 5, 1, 1), ("40", "8")),
+                                               # z-edge tiles first (mode bit 32) on one-sided corner ranks
+                                               (8, (34, 66, 136, 5, 0, 0), ("42", "44"))])
 def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
     # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
