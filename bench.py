@@ -70,7 +70,9 @@ FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 
 FUSED_DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
 # f32 (1024^3 config): tiling 14 with the edge-lane z exchange (fused variant
 # 44) is the fastest fused form there (profiles/r2_f32_fused/).
-FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4))
+FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4), (44, 36, 4))
+# (send mode bit 32 = z-edge tiles dispatched first: the f32 2x2x2 corner's best
+# form at 4 grid rounds; slower for f64 at every round count, profiles/r4_shapes/)
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")

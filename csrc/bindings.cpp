@@ -277,6 +277,10 @@ PYBIND11_MODULE(_igg_native, m) {
     IGG_HIP_CHECK(hipMemcpy(out.data(), reinterpret_cast<void*>(src), n, hipMemcpyDeviceToHost));
     return py::bytes(out);
   });
+  m.def("clear_last_error", []() {
+    const hipError_t e = hipGetLastError();  // reads and resets the thread's sticky error
+    return e == hipSuccess ? std::string() : std::string(hipGetErrorString(e));
+  }, "Reset the HIP runtime's last-error state (after a failed capture); returns the error it held.");
   m.def("rccl_version", &rccl_version);
   m.def("abandoned_waits", &abandoned_waits,
         "Bounded first-contact calls this process gave up on (their helper threads are still stuck in the "

@@ -30,7 +30,7 @@ import torch
 from .. import parallel  # noqa: F401
 from .._native import native
 from ..parallel import grid as _grid
-from ..parallel.halo import register_graph, update_halo_
+from ..parallel.halo import capture_graph, update_halo_
 from .diffusion3d import GRAPH_STEPS
 from ..utils.tools import coords_g, nx_g, ny_g
 
@@ -203,13 +203,13 @@ class Acoustic2D:
             raise ValueError("Acoustic2D.capture: steps must be even and >= 2")
         if not self._warm or (self.fused and self._entry):
             self.step()  # the graph holds steady-state steps only (no entry barrier)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        def record():
             for _ in range(steps):
                 self._step()  # no exit barrier inside the graph: run() drains once
-        torch.cuda.synchronize()
-        register_graph(g)
+
+        self.graph = None
+        # fused steps exchange through their own peer mesh, not update_halo_
+        g = capture_graph(record, f"{type(self).__name__}.capture", uses_halo=not self.fused)
         self.graph = g
         self.graph_steps = steps
         self._graph_P = self.P.data_ptr()

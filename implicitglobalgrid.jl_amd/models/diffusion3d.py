@@ -38,7 +38,7 @@ import torch
 from .. import parallel  # noqa: F401
 from ..ops import stencil
 from ..parallel import grid as _grid
-from ..parallel.halo import register_graph, update_halo_
+from ..parallel.halo import capture_graph, update_halo_
 from ..utils.tools import coords_g, nx_g, ny_g, nz_g
 
 
@@ -407,13 +407,13 @@ class Diffusion3D:
             self.step()
         if self.fused and not self._fprimed:
             self.step()  # captured fused steps read the arena: it must hold T's halos
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        def record():
             for _ in range(steps):
                 self._step()  # no exit barrier inside the graph: run() drains once
-        torch.cuda.synchronize()
-        register_graph(g)
+
+        self.graph = None
+        # fused steps exchange through their own peer mesh, not update_halo_
+        g = capture_graph(record, f"{type(self).__name__}.capture", uses_halo=not self.fused)
         self.graph = g
         self.graph_steps = steps
         self._graph_fused = self.fused

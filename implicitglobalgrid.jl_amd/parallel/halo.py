@@ -265,6 +265,50 @@ def abort_loopback() -> None:
             pass
 
 
+# Device transports whose exchanges can be recorded in a hipGraph: RCCL
+# (grouped ncclSend/ncclRecv on the stream) and put (kernels + device-side
+# flags). 'gloo-staged' and 'torch-nccl' synchronise with the host inside an
+# exchange.
+CAPTURABLE = ("rccl", "put", "none")
+
+
+def capturable() -> bool:
+    """Whether ``update_halo_`` of device fields can be captured in a hipGraph
+    with the current transport (single-process grids: always)."""
+    if _loopback_comm is not None:
+        return _engine.transport_name(True) in CAPTURABLE
+    if _grid.global_grid().nprocs == 1:
+        return True
+    return transport_name() in CAPTURABLE
+
+
+def capture_graph(record, what: str, uses_halo: bool = True):
+    """A hipGraph of ``record()`` (which enqueues work on the current stream).
+    Raises IGGError before beginning if the halo transport cannot be captured.
+    If the capture fails, the runtime's sticky error from the failed capture is
+    reset, so the next kernel launch does not report it (round 4: a rehearsal
+    with the host-staged transport died at the first eager step after a failed
+    capture)."""
+    if uses_halo and not capturable():
+        raise IGGError(f"{what}: the '{transport_name()}' transport synchronises with the host inside an exchange "
+                       "and cannot be captured in a hipGraph; run eager steps")
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            record()
+    except Exception:
+        try:
+            torch.cuda.synchronize()
+        except Exception:
+            pass
+        native.clear_last_error()
+        raise
+    torch.cuda.synchronize()
+    register_graph(g)
+    return g
+
+
 def engine():
     _grid.check_initialized()
     return _engine
