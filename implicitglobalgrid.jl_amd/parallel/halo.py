@@ -216,6 +216,7 @@ def set_transport(name: str) -> None:
     """Switch the device transport of ``update_halo_`` ('rccl', 'put', 'torch'
     or 'staged'). Collective: every rank must switch at the same point (the
     first use of a transport creates its communicator / peer mesh)."""
+    name = {v: k for k, v in _PENDING_NAMES.items()}.get(name, name)  # transport_name() spellings too
     gg = _grid.global_grid()
     if gg.nprocs == 1:
         raise IGGError("set_transport: a single-process grid has no device transport")
