@@ -188,6 +188,7 @@ def free_port(host: str = "127.0.0.1") -> int:
 
 def _stop(procs: list, grace: float = 10.0) -> None:
     """Stop exact child process groups (never by pattern)."""
+    procs = list(procs)
     for p in procs:
         if p is not None and p.poll() is None:
             try:
@@ -206,10 +207,34 @@ def _stop(procs: list, grace: float = 10.0) -> None:
             except OSError:
                 pass
             p.wait()
+    for p in procs:
+        if p in _LIVE:
+            _LIVE.remove(p)
+
+
+_LIVE: list = []  # worker processes of this supervisor (stopped if it is terminated)
+
+
+def _on_term(signum, frame) -> None:
+    """A supervisor that is told to stop (the launcher tearing the job down,
+    a driver timeout) first stops its workers: they run in their own process
+    groups and would otherwise keep the GPU."""
+    _stop(_LIVE, grace=5.0)
+    raise SystemExit(128 + signum)
+
+
+def _install_term_handler() -> None:
+    for sig in (signal.SIGTERM, signal.SIGHUP):
+        try:
+            signal.signal(sig, _on_term)
+        except (ValueError, OSError):  # not the main thread
+            pass
 
 
 def _spawn(argv: list, env: dict, out) -> subprocess.Popen:
-    return subprocess.Popen(argv, env=env, stdout=out, stderr=None, start_new_session=True)
+    p = subprocess.Popen(argv, env=env, stdout=out, stderr=None, start_new_session=True)
+    _LIVE.append(p)
+    return p
 
 
 def _result_line(out) -> tuple[str | None, list]:
@@ -234,6 +259,14 @@ def run_local(argv: list, n: int, base_env: dict, *, max_attempts: int = 4, time
 
     Returns (exit code, rank 0's result line or None, {key: reason} excluded).
     ``env_for_rank(r, env)`` may adjust a rank's environment."""
+    _install_term_handler()
+    try:
+        return _run_local(argv, n, base_env, max_attempts, timeout, env_for_rank, poll)
+    finally:
+        _stop(_LIVE)  # whatever ended the supervision, no worker outlives it
+
+
+def _run_local(argv, n, base_env, max_attempts, timeout, env_for_rank, poll):
     excl = excluded(base_env)
     t_end = time.monotonic() + timeout
     tmp = tempfile.mkdtemp(prefix="igg_sup_")
@@ -335,6 +368,14 @@ def run_torchrun(argv: list, *, max_attempts: int = 4, timeout: float = 1800.0, 
     rank/world and a per-attempt rendezvous port, and agrees with the other
     supervisors over the launcher's TCP store on done / relaunch / fail.
     Supervisor 0 decides; rank 0's supervisor prints the result line."""
+    _install_term_handler()
+    try:
+        return _run_torchrun(argv, max_attempts, timeout, poll, env_adjust)
+    finally:
+        _stop(_LIVE)
+
+
+def _run_torchrun(argv, max_attempts, timeout, poll, env_adjust):
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     g = _StoreGroup(rank, size)
     excl = excluded()

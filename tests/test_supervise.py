@@ -143,3 +143,41 @@ def test_torchrun_supervisors_survive_an_injected_hang():
     assert rec["n_gpus"] == 2 and rec["config"]["self_launched"] is False
     assert "host-ordered" in rec["config"]["excluded"]
     assert rec["config"]["supervisor_attempt"] == 1
+
+
+def test_terminated_supervisor_stops_its_workers():
+    """The launcher (or a driver timeout) terminating the self-launch parent
+    must not leave its worker ranks running - they hold the GPU."""
+    import signal
+    import time
+    import uuid
+
+    marker = uuid.uuid4().hex
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", *ARGS], stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, cwd=ROOT,
+                         env=_env(IGG_INJECT_PHASE_HANG="model@0", IGG_TEST_MARKER=marker))
+
+    def workers():
+        out = []
+        for pid in os.listdir("/proc"):
+            if not pid.isdigit() or int(pid) == p.pid:
+                continue
+            try:
+                with open(f"/proc/{pid}/environ", "rb") as f:
+                    if f"IGG_TEST_MARKER={marker}".encode() in f.read() and b"IGG_SUP_CHILD=1" in open(
+                            f"/proc/{pid}/environ", "rb").read():
+                        out.append(int(pid))
+            except OSError:
+                pass
+        return out
+
+    t0 = time.monotonic()
+    while len(workers()) < 2 and time.monotonic() - t0 < 60:
+        time.sleep(0.5)
+    assert len(workers()) == 2, "the workers did not start"
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=60)
+    t1 = time.monotonic()
+    while workers() and time.monotonic() - t1 < 20:
+        time.sleep(0.5)
+    assert workers() == [], "workers outlived their terminated supervisor"
