@@ -97,20 +97,17 @@ class Diffusion3D:
         x = coords_g(0, self.dx, probe, **kw).view(-1, 1, 1)
         y = coords_g(1, self.dy, probe, **kw).view(1, -1, 1)
         z = coords_g(2, self.dz, probe, **kw).view(1, 1, -1)
-        self.Cp = (cp_min + 5 * torch.exp(-(x - lx / 1.5) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2)
-                   + 5 * torch.exp(-(x - lx / 3.0) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2)).to(dtype).contiguous()
-        self.T = (100 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 3.0) / 2) ** 2)
-                  + 50 * torch.exp(-((x - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2 - ((z - lz / 1.5) / 2) ** 2)).to(dtype).contiguous()
-        self.T2 = self.T.clone()
-        # One allocation with gaps between the three arrays: measured 1-3 %
-        # faster than back-to-back 2 MiB-aligned tensors on MI355X
-        # (profiles/r2_offsets/stencil_offsets.py: HBM channel placement).
         # field_memory (IGG_FIELD_MEMORY): "fine" (default: one native
         # fine-grained allocation) or "torch" (coarse-grained, torch's caching
         # allocator). The direct-z fused exchange stores into the neighbours'
         # T/T2 while their kernels run, which HIP defines for fine-grained
         # memory only (docs/COHERENCE.md); the plain sweep runs as fast on it
         # (profiles/r3_coherence/: 0.6222 vs 0.6263 ms/step).
+        # One allocation with gaps between the three arrays: measured 1-3 %
+        # faster than back-to-back 2 MiB-aligned tensors on MI355X
+        # (profiles/r2_offsets/stencil_offsets.py: HBM channel placement). The
+        # fields are allocated first and the initial conditions written into
+        # them (no full-size temporary copies).
         import os as _os
 
         self.field_memory = (field_memory or _os.environ.get("IGG_FIELD_MEMORY", "fine")).strip().lower()
@@ -120,9 +117,27 @@ class Diffusion3D:
             # With neighbours in other processes T/T2 may be IPC-mapped (direct
             # z, gather_ pull): no allocation may reach the IPC size limit, so
             # a carve that would is split into one allocation per array.
-            self.T, self.Cp, self.T2 = _carve([self.T, self.Cp, self.T2], gap=266240,
-                                              kind=1 if self.field_memory == "fine" else None,
-                                              split_at=_ipc_limit() if int(gg.nprocs) > 1 else None)
+            spec = [torch.empty(shape, dtype=dtype, device="meta")] * 3
+            self.T, self.Cp, self.T2 = _carve(spec, gap=266240, kind=1 if self.field_memory == "fine" else None,
+                                              split_at=_ipc_limit() if int(gg.nprocs) > 1 else None,
+                                              device=self.device)
+        else:
+            self.T, self.Cp, self.T2 = (torch.empty(shape, dtype=dtype) for _ in range(3))
+        # Gaussian anomalies, evaluated in float64 a slab of x planes at a time
+        # into the target dtype: the float64 temporaries of the whole field
+        # (several x 8 bytes per point) would otherwise be the memory peak of a
+        # 1024^3 rank - 8 ranks sharing one GPU ran out of memory here - while
+        # every value is the same elementwise expression as before.
+        slab = max(1, (1 << 24) // max(1, ny * nz))
+        for x0 in range(0, nx, slab):
+            xs = x[x0:x0 + slab]
+            self.Cp[x0:x0 + slab] = (cp_min + 5 * torch.exp(-(xs - lx / 1.5) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2)
+                                     + 5 * torch.exp(-(xs - lx / 3.0) ** 2 - (y - ly / 2) ** 2 - (z - lz / 1.5) ** 2))
+            self.T[x0:x0 + slab] = (100 * torch.exp(-((xs - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2
+                                                    - ((z - lz / 3.0) / 2) ** 2)
+                                    + 50 * torch.exp(-((xs - lx / 2) / 2) ** 2 - ((y - ly / 2) / 2) ** 2
+                                                     - ((z - lz / 1.5) / 2) ** 2))
+        self.T2.copy_(self.T)
         sides = [[bool(gg.neighbors[0, d] != -1), bool(gg.neighbors[1, d] != -1)] for d in range(3)]
         self.sides = sides
         self.can_overlap = self.device.type == "cuda" and any(any(sd) for sd in sides)
@@ -490,24 +505,27 @@ def _ipc_limit() -> int:
     return int(native.IPC_MAX_BYTES)
 
 
-def _carve(tensors, gap: int, kind=None, split_at=None):
+def _carve(tensors, gap: int, kind=None, split_at=None, device=None):
     """Copies of equally sized tensors placed in one buffer ``gap`` bytes apart.
     ``kind``: None = torch's caching allocator, else a native MemKind (1 =
     fine-grained) allocated by the runtime and handed over through DLPack.
     ``split_at``: if the one buffer would reach this many bytes, one
-    allocation per tensor instead (the IPC size limit)."""
+    allocation per tensor instead (the IPC size limit). Meta tensors give
+    shape and dtype only: uninitialised views on ``device``."""
     nbytes = tensors[0].numel() * tensors[0].element_size()
     stride = nbytes + gap
+    device = tensors[0].device if device is None else device
     if split_at is not None and stride * len(tensors) >= split_at and len(tensors) > 1:
-        return [_carve([t], 0, kind)[0] for t in tensors]
+        return [_carve([t], 0, kind, device=device)[0] for t in tensors]
     if kind is None:
-        buf = torch.empty(stride * len(tensors), dtype=torch.uint8, device=tensors[0].device)
+        buf = torch.empty(stride * len(tensors), dtype=torch.uint8, device=device)
     else:
-        buf = native_buffer(stride * len(tensors), kind, tensors[0].device)
+        buf = native_buffer(stride * len(tensors), kind, device)
     out = []
     for k, t in enumerate(tensors):
         v = buf[k * stride:k * stride + nbytes].view(t.dtype).view(t.shape)
-        v.copy_(t)
+        if t.device.type != "meta":
+            v.copy_(t)
         out.append(v)
     return out
 
