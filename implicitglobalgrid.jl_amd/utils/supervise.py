@@ -288,6 +288,7 @@ def _run_local(argv, n, base_env, max_attempts, timeout, env_for_rank, poll):
             outs.append(out)
             procs.append(_spawn(argv, env, out))
         exit_t = [None] * n
+        t_start = time.time()  # a rank that never wrote a phase is "starting" since the launch
         verdict = None
         try:
             while verdict is None:
@@ -302,7 +303,8 @@ def _run_local(argv, n, base_env, max_attempts, timeout, env_for_rank, poll):
                         s.update(exit=c, exit_t=exit_t[r])
                     else:
                         s["exit"] = None
-                        s.setdefault("since", now)
+                        s.setdefault("phase", "start")
+                        s.setdefault("since", t_start)
                         s.setdefault("deadline", DEFAULT_DEADLINE)
                     st.append(s)
                 verdict = decide(st, now, excl, max_attempts - attempt)
@@ -400,6 +402,7 @@ def _run_torchrun(argv, max_attempts, timeout, poll, env_adjust):
         out = tempfile.TemporaryFile(mode="w+")
         p = _spawn(argv, env, out)
         exit_t, last_pub, verdict = None, None, None
+        t_start = time.time()
         while verdict is None:
             now = time.time()
             s = _read_phase(env["IGG_PHASE_FILE"])
@@ -409,6 +412,8 @@ def _run_torchrun(argv, max_attempts, timeout, poll, env_adjust):
                 s.update(exit=c, exit_t=exit_t)
             else:
                 s["exit"] = None
+                if "since" not in s:  # no phase written yet: starting since the launch
+                    s.update(phase="start", since=t_start, deadline=DEFAULT_DEADLINE)
             pub = json.dumps(s, sort_keys=True)
             if pub != last_pub:
                 g.set(f"a{attempt}/s{rank}", s)
