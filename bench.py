@@ -337,9 +337,16 @@ def _probe_field(field):
     from igg.parallel.grid import global_grid
 
     me = int(global_grid().me)
-    X = torch.arange(field.numel(), dtype=torch.float64, device=field.device).view(field.shape)
-    X += float(me + 1) * 2.0 ** 30
-    X = X.to(field.dtype)
+    # built a slab of the outermost dim at a time (no field-size float64
+    # temporary: 8 ranks x 1024^3 sharing one GPU ran out of memory here)
+    X = torch.empty_like(field)
+    n0 = field.shape[0]
+    per = max(1, field.numel() // max(1, n0))
+    slab = max(1, (1 << 24) // per)
+    for a in range(0, n0, slab):
+        b = min(n0, a + slab)
+        v = torch.arange(a * per, b * per, dtype=torch.float64, device=field.device) + float(me + 1) * 2.0 ** 30
+        X[a:b] = v.view((b - a,) + tuple(field.shape[1:]))
     for d in range(field.dim()):
         X.select(d, 0).fill_(-7.0)
         X.select(d, field.shape[d] - 1).fill_(-7.0)
@@ -360,10 +367,11 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
 
     from igg.parallel import halo as H
 
-    X0 = _probe_field(field)
+    # two field-size buffers at a time: the reference R and the candidate's X
+    # (the probe is regenerated, not kept)
     H.set_transport(ref)
     H.set_halo_mode("sequential")
-    R = X0.clone()
+    R = _probe_field(field)
     H.update_halo_(R)
     _sync(comm)
     out = {}
@@ -381,7 +389,7 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
         try:
             H.set_transport(t)  # collective: creates the RCCL communicator / put mesh on first use
             H.set_halo_mode(mode)
-            X = X0.clone()
+            X = _probe_field(field)
             H.update_halo_(X)
             _sync(comm)
             H.check_transport()
@@ -399,7 +407,7 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
         _check_abandoned(comm, key, f"validation of {name}", log)
     H.set_transport("rccl" if out.get("rccl-sequential") == "ok" else ref)
     H.set_halo_mode("auto")
-    del X0, R
+    del R
     return out
 
 
@@ -414,7 +422,6 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
 
     from igg.parallel import halo as H
 
-    X0 = _probe_field(field)
     if on_gpu:
         t, gmode = H.transport_name(), H.halo_mode()
         sched = "put" if t == "put" else H.plan_mode(field)
@@ -429,7 +436,7 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
     try:
         if on_gpu and t != "put":
             H.set_halo_mode(sched)
-        X = X0.clone()
+        X = _probe_field(field)
         H.update_halo_(X)
         if on_gpu:
             _sync(comm)
@@ -439,7 +446,7 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
             H.set_halo_mode("sequential")
         elif f"host-{other}" not in EXCL:
             os.environ["IGG_HOST_MATCHING"] = other
-        R = X0.clone()
+        R = _probe_field(field)
         H.update_halo_(R)
         if on_gpu:
             _sync(comm)
@@ -451,11 +458,11 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
         if os.environ.get("IGG_BENCH_DEBUG_POST") and on_gpu:  # which side is wrong (diagnostics; collective)
             from igg.parallel.grid import global_grid
 
-            R2 = X0.clone()
+            R2 = _probe_field(field)
             H.update_halo_(R2)
             _sync(comm)
             H.set_transport(t)
-            X2 = X0.clone()
+            X2 = _probe_field(field)
             H.update_halo_(X2)
             _sync(comm)
             H.set_transport("staged")
@@ -683,9 +690,27 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
             t_unf = min(t_unf, _timed_candidate(model, comm, 20, graph))
             model.set_fused(True)
             for c in cs:
+                if times.get(c) == float("inf"):
+                    continue  # failed in the first pass
                 use(c)
                 PH.enter(f"fused:ab:{name(c)}", ckey(c), deadline=300)
-                t = _timed_candidate(model, comm, 20, graph)
+                err = ""
+                try:
+                    t = _timed_candidate(model, comm, 20, graph)
+                except Exception as e:  # this form cannot run here (e.g. a bounded wait expired)
+                    t, err = float("inf"), f"{type(e).__name__}: {e}"[:200]
+                if _max_over_ranks(comm, 1.0 if err else 0.0):
+                    # every rank drops the form together; a neighbour's timed-out
+                    # waits left the sticky error word set: drain and reset it
+                    log(f"fused candidate {name(c)} failed: {err or 'on another rank'}")
+                    try:
+                        _sync(comm)
+                    except Exception:
+                        pass
+                    if hasattr(model, "clear_error"):
+                        model.clear_error()
+                    model.graph = None
+                    t = float("inf")
                 times[c] = min(times.get(c, float("inf")), t)
 
     timing_passes(cands)
@@ -704,7 +729,7 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
     model.graph = None
     keep, best, rejected = False, None, []
     for cand, t_fus in sorted(times.items(), key=lambda kv: kv[1]):
-        if not (mode == "on" or t_fus < t_unf):
+        if t_fus == float("inf") or not (mode == "on" or t_fus < t_unf):
             break
         use(cand)
         # the kept candidate: a long check whatever the quick one said
@@ -723,7 +748,7 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
         + (f" (failed their bitwise check: {', '.join(rejected)})" if rejected else ""))
     out = {"fused_ok": True, "update_halo": round(t_unf * 1e3, 5),
            "kept_check_steps": FUSED_KEEP_CHECK_STEPS if keep else None}
-    out.update({f"fused_{name(k)}": round(t * 1e3, 5) for k, t in times.items()})
+    out.update({f"fused_{name(k)}": (round(t * 1e3, 5) if t != float("inf") else None) for k, t in times.items()})
     if rejected:
         out["fused_rejected"] = rejected
     return out

@@ -334,15 +334,19 @@ class Diffusion3D:
         if self.fused:
             rd2 = [1.0 / self.dx ** 2, 1.0 / self.dy ** 2, 1.0 / self.dz ** 2]
             s = torch.cuda.current_stream().cuda_stream
+            # direct z (bit 4) needs the registered field buffers; where they
+            # could not be mapped (fields above the IPC limit) the same form
+            # runs with the arena z exchange
+            mode = self.fused_mode if self._fh.has_fields else self.fused_mode & ~4
             if self.timer is not None:
                 with self.timer.phase("stencil+exchange"):
                     self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
                                   self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
-                                  self.fused_mode, self._fentry)
+                                  mode, self._fentry)
             else:
                 self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
                               self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
-                              self.fused_mode, self._fentry)
+                              mode, self._fentry)
             self._fentry = False
             self._fstep += 1
             self._fprimed = True
