@@ -284,6 +284,8 @@ def _step_estimate_ms(model, comm) -> float:
 
 
 class _NoPhases:
+    supervised = False
+
     def enter(self, *a, **k):
         pass
 
@@ -586,7 +588,7 @@ def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = 
     model.run(nchk)
     ref = {n: getattr(model, n).clone() for n in names}
     restore()
-    ok = False
+    ok, exc = False, ""
     try:
         model.set_fused(True)
         model.step()
@@ -610,9 +612,19 @@ def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = 
             print(f"rank {int(global_grid().me)}: fused check {_fused_name(model)}: {n} differs in "
                   f"{d.shape[0]} entries, first {d[:4].tolist()}", file=sys.stderr, flush=True)
     except Exception as e:  # e.g. a sync kernel timed out: this fused kernel does not work here
-        log(f"fused check {_fused_name(model)} failed: {type(e).__name__}: {e}"[:300])
+        exc = f"{type(e).__name__}: {e}"[:300]
+        from igg.parallel.grid import global_grid
+
+        print(f"rank {int(global_grid().me)}: fused check {_fused_name(model)} failed: {exc}", file=sys.stderr,
+              flush=True)
         if getattr(comm, "mesh", None) is not None:
             comm.mesh.clear_error()
+    if _max_over_ranks(comm, 1.0 if exc else 0.0) and PH.supervised:
+        # An exception in the middle of collective steps (a timeout, out of
+        # memory) can leave the ranks' exchange counters out of step: not a
+        # state to continue from. Fresh processes without this form instead.
+        key = "fused-inkernel" if getattr(model, "fused_mode", 0) & 16 else "fused"
+        PH.relaunch({key: f"fused check {_fused_name(model)} raised on some rank ({exc or 'another rank'})"})
     bad = _max_over_ranks(comm, 0.0 if ok else 1.0)
     if bad:
         # A timed-out fused step leaves the fused mesh's sticky error word set
@@ -700,6 +712,8 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
                 except Exception as e:  # this form cannot run here (e.g. a bounded wait expired)
                     t, err = float("inf"), f"{type(e).__name__}: {e}"[:200]
                 if _max_over_ranks(comm, 1.0 if err else 0.0):
+                    if PH.supervised:  # fresh processes without this class of forms (see _fused_check)
+                        PH.relaunch({ckey(c): f"fused candidate {name(c)} raised on some rank ({err or 'another'})"})
                     # every rank drops the form together; a neighbour's timed-out
                     # waits left the sticky error word set: drain and reset it
                     log(f"fused candidate {name(c)} failed: {err or 'on another rank'}")

@@ -70,6 +70,7 @@ class Phases:
 
     def __init__(self, rank: int | None = None):
         self.path = os.environ.get("IGG_PHASE_FILE")
+        self.supervised = self.path is not None
         self.rank = int(os.environ.get("RANK", "0")) if rank is None else rank
         self.attempt = int(os.environ.get("IGG_SUP_ATTEMPT", "0"))
         self.scale = float(os.environ.get("IGG_PHASE_DEADLINE_SCALE", "1"))
@@ -87,6 +88,8 @@ class Phases:
         self.cur = {"phase": name, "key": key, "since": time.time(), "deadline": float(deadline) * self.scale,
                     "pid": os.getpid()}
         self._write(self.cur)
+        if self.rank == 0 and self.path:  # progress on stderr (and never a silent minute)
+            print(f"[phase] {name}" + (f" (path {key})" if key else ""), file=sys.stderr, flush=True)
         self._maybe_hang(name)
 
     def printed(self) -> None:
