@@ -369,13 +369,15 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
 
     from igg.parallel import halo as H
 
-    # two field-size buffers at a time: the reference R and the candidate's X
-    # (the probe is regenerated, not kept)
+    # the reference's boundary planes only (the only entries an exchange
+    # writes), and one field-size probe at a time
     H.set_transport(ref)
     H.set_halo_mode("sequential")
     R = _probe_field(field)
     H.update_halo_(R)
     _sync(comm)
+    Rb = _boundary(R)
+    del R
     out = {}
     for name, t, mode in TRANSPORT_CANDIDATES:
         if names is not None and name not in names:
@@ -387,37 +389,64 @@ def validate_transports(field, comm, log, ref: str = "staged", names=None) -> di
             continue
         # deadline: a bounded first contact (IGG_FIRST_CONTACT_TIMEOUT) + the exchange
         PH.enter(f"validate:{name}", key, deadline=2 * _first_contact() + 120)
-        why = ""
+        why, X = "", None
         try:
-            H.set_transport(t)  # collective: creates the RCCL communicator / put mesh on first use
+            H.set_transport(t)  # collective (outcome agreed): creates the RCCL communicator / put mesh
             H.set_halo_mode(mode)
             X = _probe_field(field)
-            H.update_halo_(X)
-            _sync(comm)
-            H.check_transport()
-            if not torch.equal(X, R):
-                bad = (X != R).nonzero()
-                why = f"mismatch at {bad.shape[0]} entries, first {bad[0].tolist()}"
-            del X
-        except Exception as e:  # e.g. no IPC mapping between these GPUs, a bounded spin timed out
+        except Exception as e:  # e.g. no IPC mapping between these GPUs
             why = f"{type(e).__name__}: {e}"[:300]
-            if getattr(comm, "mesh", None) is not None:
-                comm.mesh.clear_error()
+        if _all_ok(comm, why):  # every rank has its probe: the exchange can start
+            try:
+                H.update_halo_(X)
+                _sync(comm)
+                H.check_transport()
+                for k, (a, b) in enumerate(zip(_boundary(X), Rb)):
+                    if not torch.equal(a, b):
+                        bad = (a != b).nonzero()
+                        why = f"mismatch in boundary plane {k} at {bad.shape[0]} entries, first {bad[0].tolist()}"
+                        break
+            except Exception as e:  # a bounded spin timed out, a transport error
+                why = f"{type(e).__name__}: {e}"[:300]
+                if getattr(comm, "mesh", None) is not None:
+                    comm.mesh.clear_error()
+        X = None
         fails = _max_over_ranks(comm, 1.0 if why else 0.0)
         out[name] = "ok" if fails == 0.0 else (why or "failed on another rank")
         log(f"validation {name} vs {ref}: {out[name]}")
         _check_abandoned(comm, key, f"validation of {name}", log)
     H.set_transport("rccl" if out.get("rccl-sequential") == "ok" else ref)
     H.set_halo_mode("auto")
-    del R
     return out
+
+
+def _boundary(X) -> list:
+    """Copies of the boundary planes of ``X`` (index 0 and n-1 of every dim):
+    the only entries a halo update writes (the halo is one plane wide whatever
+    the overlap, SURVEY invariant 2) - compared instead of whole probe copies."""
+    out = []
+    for d in range(X.dim()):
+        out.append(X.select(d, 0).clone())
+        if X.shape[d] > 1:
+            out.append(X.select(d, X.shape[d] - 1).clone())
+    return out
+
+
+def _all_ok(comm, why: str) -> bool:
+    """Collective: True iff no rank reported a failure. Called between the
+    collective stages of a check, so one rank's local failure (an allocation,
+    a transport error before its messages were posted) never leaves the others
+    waiting inside the next exchange."""
+    return _max_over_ranks(comm, 1.0 if why else 0.0) == 0.0
 
 
 def post_validate(field, comm, log, on_gpu: bool) -> dict:
     """After the timed region: one update_halo_ of the probe payload through
     the transport and schedule the timed steps used, compared bitwise with the
     host-staged gloo exchange (the reference's non-GPU-aware path). Collective;
-    every rank agrees. The transport / schedule settings are restored.
+    every rank agrees, stage by stage. The transport / schedule settings are
+    restored. At most one field-size probe exists at a time (8 ranks of
+    1024^3 f32 sharing one GPU ran out of memory with three).
     (CPU plumbing runs: the timed host matching form against the other one,
     order-only vs tagged, unless that one is excluded.)"""
     import torch
@@ -431,50 +460,62 @@ def post_validate(field, comm, log, on_gpu: bool) -> dict:
         m = os.environ.get("IGG_HOST_MATCHING", "ordered")
         t, gmode, sched = f"host-{m}", None, "sequential"
         other = "tagged" if m == "ordered" else "ordered"
-    why = ""
-    if os.environ.get("IGG_BENCH_DEBUG_POST") and on_gpu and t == "put":  # diagnostics (collective)
-        eps = comm.all_gather_object(int(comm.mesh.epoch))
-        log(f"post-timing validation: put epochs per rank before the probe exchange: {eps}")
-    try:
-        if on_gpu and t != "put":
-            H.set_halo_mode(sched)
-        X = _probe_field(field)
-        H.update_halo_(X)
-        if on_gpu:
-            _sync(comm)
-        H.check_transport()
-        if on_gpu:
-            H.set_transport("staged")
-            H.set_halo_mode("sequential")
-        elif f"host-{other}" not in EXCL:
-            os.environ["IGG_HOST_MATCHING"] = other
-        R = _probe_field(field)
-        H.update_halo_(R)
-        if on_gpu:
-            _sync(comm)
-        if _inject("post_validation"):
-            X.view(-1)[X.numel() // 2] += 1
-        if not torch.equal(X, R):
-            bad = (X != R).nonzero()
-            why = f"mismatch at {bad.shape[0]} entries, first {bad[0].tolist()}"
-        if os.environ.get("IGG_BENCH_DEBUG_POST") and on_gpu:  # which side is wrong (diagnostics; collective)
-            from igg.parallel.grid import global_grid
+    why, Xb = "", None
 
-            R2 = _probe_field(field)
-            H.update_halo_(R2)
-            _sync(comm)
-            H.set_transport(t)
-            X2 = _probe_field(field)
-            H.update_halo_(X2)
-            _sync(comm)
-            H.set_transport("staged")
-            print(f"rank {int(global_grid().me)}: ok {not why}; staged again == staged {torch.equal(R, R2)}, "
-                  f"put again == put {torch.equal(X, X2)}, put again == staged {torch.equal(X2, R)}; {why}",
-                  file=sys.stderr, flush=True)
-    except Exception as e:  # a bounded wait expired, a transport error
-        why = f"{type(e).__name__}: {e}"[:300]
+    def err(e) -> str:
         if getattr(comm, "mesh", None) is not None:
-            comm.mesh.clear_error()
+            try:
+                comm.mesh.clear_error()
+            except Exception:
+                pass
+        return f"{type(e).__name__}: {e}"[:300]
+
+    try:
+        X = None
+        try:
+            if on_gpu and t != "put":
+                H.set_halo_mode(sched)
+            X = _probe_field(field)
+        except Exception as e:
+            why = err(e)
+        if _all_ok(comm, why):
+            try:  # the timed path
+                H.update_halo_(X)
+                if on_gpu:
+                    _sync(comm)
+                H.check_transport()
+                Xb = _boundary(X)
+            except Exception as e:  # a bounded wait expired, a transport error
+                why = err(e)
+            X = None
+        R = None
+        if _all_ok(comm, why):
+            try:  # the reference path
+                if on_gpu:
+                    H.set_transport("staged")
+                    H.set_halo_mode("sequential")
+                elif f"host-{other}" not in EXCL:
+                    os.environ["IGG_HOST_MATCHING"] = other
+                R = _probe_field(field)
+            except Exception as e:
+                why = err(e)
+        if _all_ok(comm, why):
+            try:
+                H.update_halo_(R)
+                if on_gpu:
+                    _sync(comm)
+                Rb = _boundary(R)
+                R = None
+                if _inject("post_validation"):
+                    Xb[0].view(-1)[Xb[0].numel() // 2] += 1
+                for k, (a, b) in enumerate(zip(Xb, Rb)):
+                    if not torch.equal(a, b):
+                        bad = (a != b).nonzero()
+                        why = (f"mismatch in boundary plane {k} (dim {k // 2}) at {bad.shape[0]} entries, "
+                               f"first {bad[0].tolist()}")
+                        break
+            except Exception as e:
+                why = err(e)
     finally:
         if on_gpu:
             H.set_transport(t)
@@ -799,10 +840,17 @@ def stencil_post_check(model, comm, log, pre: dict, k: int, on_gpu: bool) -> dic
     import torch
 
     names = _state(model)
-    done = {n: getattr(model, n).clone() for n in names}
     v_timed, graph = getattr(model, "variant", None), model.graph
     v2 = _second_variant(model) if on_gpu else None
-    why = ""
+    why, done = "", None
+    try:
+        done = {n: getattr(model, n).clone() for n in names}
+    except Exception as e:  # e.g. out of memory: every rank skips the re-run together
+        why = f"{type(e).__name__}: {e}"[:300]
+    if not _all_ok(comm, why):
+        res = why or "failed on another rank"
+        log(f"post-timing stencil check: could not start ({res})")
+        return {"steps": k, "variant": v_timed, "check_variant": v2, "result": res}
     try:
         for n in names:
             getattr(model, n).copy_(pre[n])
