@@ -1091,6 +1091,7 @@ def main():
         extra = int(-(-warm_ms // (est * k))) * k
         model.run(extra)
     pre = {}  # the state a non-fused timed region starts from (stencil_post_check)
+    timed_graph = [False]  # whether the last timed region replayed a hipGraph
 
     def timed_region() -> float:
         """The timed region: exactly ``args.steps`` full steps (plus the
@@ -1102,6 +1103,7 @@ def main():
             _save_start(model, pre)
         else:
             pre.clear()
+        timed_graph[0] = getattr(model, "graph", None) is not None
         sync()
         _bracket(comm)
         t0 = time.perf_counter()
@@ -1287,7 +1289,7 @@ def main():
                 "loopback_emulation": bool(args.loopback),
                 "self_launched": os.environ.get("IGG_BENCH_SELF_LAUNCHED") == "1",
                 "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                "hip_graph": getattr(model, "graph", None) is not None,
+                "hip_graph": timed_graph[0],
                 "hip_graph_error": graph_error,
                 "timing_bracket": ("rccl all-reduce + stream event + synchronize" if _BRACKET["dev"] and nprocs > 1
                                    else ("host barrier + stream event + synchronize" if on_gpu else "host barrier")),
