@@ -107,6 +107,8 @@ class Acoustic2D:
             return False
         if int(gg.overlaps[0]) != 2 or int(gg.overlaps[1]) != 2:
             return False
+        if gg.nprocs > 1 and not gg.comm.one_node:  # IPC peer mappings: one node only
+            return False
         vj = 4 if self.P.element_size() == 4 else 2
         return self.ny % vj == 0 and self.nx >= 5 and self.ny >= 5
 

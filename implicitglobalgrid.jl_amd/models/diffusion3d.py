@@ -198,6 +198,8 @@ class Diffusion3D:
             return False
         if any(any(self.sides[d]) and int(gg.overlaps[d]) != 2 for d in range(3)):
             return False
+        if gg.nprocs > 1 and not gg.comm.one_node:  # IPC peer mappings: one node only
+            return False
         return int(self.T.shape[2]) % 4 == 0 and int(self.T.shape[2]) >= 8
 
     def set_fused(self, flag: bool) -> bool:

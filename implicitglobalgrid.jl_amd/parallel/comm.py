@@ -255,6 +255,7 @@ class Communicator:
         if choice == "put":
             t = self._transports.get("put")
             if t is None:
+                self.require_one_node("the 'put' transport")
                 self.mesh = native.PeerMesh(self.rank, self.size, self._allgather_bytes)
                 t = native.PutTransport(self.mesh)
                 self._transports["put"] = t
@@ -268,6 +269,20 @@ class Communicator:
             return t
         self.ensure_rccl()
         return self.rccl
+
+    @property
+    def one_node(self) -> bool:
+        """Every rank of the communicator runs on this node (IPC peer mappings,
+        the put transport, the fused exchanges and the gather pull need it)."""
+        return self.local_size == self.size
+
+    def require_one_node(self, what: str) -> None:
+        """Raise on every rank (no collective is entered) when the ranks span
+        several nodes: IPC handles cannot be opened on another node. RCCL and
+        the staged transport work across nodes."""
+        if not self.one_node:
+            raise IGGError(f"{what} maps peer memory over IPC and needs every rank on one node "
+                           f"({self.local_size} of {self.size} ranks are on this one); use IGG_TRANSPORT=rccl")
 
     def _allgather_bytes(self, b: bytes) -> list:
         return self.all_gather_object(bytes(b))

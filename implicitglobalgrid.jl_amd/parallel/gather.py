@@ -58,7 +58,7 @@ def _pull_ok(gg, A: torch.Tensor) -> bool:
     opening a larger handle hangs on this ROCm runtime) stages ``A`` into
     exportable chunks itself (csrc/include/igg/gather.hpp PullGatherer)."""
     c = gg.comm
-    return int(gg.nprocs) > 1 and c is not None and c.local_size == c.size and config.gather_pull()
+    return int(gg.nprocs) > 1 and c is not None and c.one_node and config.gather_pull()
 
 
 def _padded_shape(A: torch.Tensor) -> list[int]:

@@ -83,3 +83,19 @@ def test_finalize_without_runtime_finalization():
         print("NOFIN OK")
     """)
     assert "NOFIN OK" in out
+
+
+def test_ipc_paths_need_one_node():
+    """Ranks on several nodes: the put transport refuses with a clear error on
+    every rank before entering any collective (IPC handles cannot be opened
+    on another node); RCCL / staged stay available."""
+    import pytest
+
+    from igg.parallel.comm import Communicator
+    from igg._native import IGGError
+
+    one = Communicator(rank=0, size=2, local_size=2)
+    two = Communicator(rank=0, size=2, local_size=1)
+    assert one.one_node and not two.one_node
+    with pytest.raises(IGGError, match="one node"):
+        two.device_transport("put")
