@@ -69,8 +69,11 @@ def main() -> int:
                     help="re-time the N fastest forms per z shape with z-edge tiles first (send mode bit 32)")
     ap.add_argument("--inkernel", type=int, default=3,
                     help="re-time the N fastest forms per shape with the in-kernel step sync (send mode bit 16)")
+    ap.add_argument("--halo-z", type=int, default=1,
+                    help="whole-line z-edge stores (DiffusionArgs::halo_z, the model's default) in plain and fused")
     a = ap.parse_args()
     n = a.n
+    hz = bool(a.halo_z)
     dt = getattr(torch, a.dtype)
     igg.init_global_grid(n, n, n, periodx=1, periody=1, periodz=1, quiet=True)
     from igg.models.diffusion3d import native_buffer
@@ -96,7 +99,7 @@ def main() -> int:
         def f():
             src, dst = bufs[k[0] & 1], bufs[(k[0] + 1) & 1]
             native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), [n, n, n], rd2, 1e-4, eb, inner, True,
-                               v, s.cuda_stream, r)
+                               v, s.cuda_stream, r, hz)
             k[0] += 1
         return f
 
@@ -105,7 +108,8 @@ def main() -> int:
 
         def f():
             src, dst = bufs[k[0] & 1], bufs[(k[0] + 1) & 1]
-            fh.step(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), rd2, 1e-4, v, k[0], True, s.cuda_stream, r, mode)
+            fh.step(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), rd2, 1e-4, v, k[0], True, s.cuda_stream, r, mode,
+                    False, hz)
             k[0] += 1
         return f
 

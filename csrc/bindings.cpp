@@ -641,9 +641,9 @@ PYBIND11_MODULE(_igg_native, m) {
   m.def("diffusion3d",
         [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
            double dtlam, int elem_bytes, const std::vector<std::pair<Int3, Int3>>& boxes,
-           bool device, int variant, uintptr_t stream, int rounds) {
+           bool device, int variant, uintptr_t stream, int rounds, bool halo_z) {
           TraceRange tr("igg.diffusion3d");
-          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes, rounds};
+          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes, rounds, halo_z};
           const auto bx = to_boxes(boxes);
           if (device) {
             launch_diffusion3d(a, bx, variant, as_stream(stream));
@@ -654,18 +654,19 @@ PYBIND11_MODULE(_igg_native, m) {
         },
         py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
         py::arg("elem_bytes"), py::arg("boxes"), py::arg("device"), py::arg("variant") = 0,
-        py::arg("stream") = 0, py::arg("rounds") = 0);
+        py::arg("stream") = 0, py::arg("rounds") = 0, py::arg("halo_z") = false);
   // Inner-box sweep through one restrict-form tiling id (fused_kernels.hip
   // dispatch_plain); the measurement-only tilings (incl. the timing probes
   // 130-132 of profiles/r2_refetch/refetch_probe.py) exist only in a --probes build.
   m.def("diffusion3d_hx_tiling",
         [](uintptr_t t2, uintptr_t t, uintptr_t cp, const Int3& n, const std::array<double, 3>& rd2,
-           double dtlam, int elem_bytes, int tiling, uintptr_t stream, int rounds) {
-          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes, rounds};
+           double dtlam, int elem_bytes, int tiling, uintptr_t stream, int rounds, bool halo_z) {
+          DiffusionArgs a{t2, t, cp, {n[0], n[1], n[2]}, {rd2[0], rd2[1], rd2[2]}, dtlam, elem_bytes, rounds, halo_z};
           launch_diffusion3d_inner_hx(a, tiling, as_stream(stream));
         },
         py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("n"), py::arg("rd2"), py::arg("dtlam"),
-        py::arg("elem_bytes"), py::arg("tiling"), py::arg("stream") = 0, py::arg("rounds") = 0);
+        py::arg("elem_bytes"), py::arg("tiling"), py::arg("stream") = 0, py::arg("rounds") = 0,
+        py::arg("halo_z") = false);
   m.def("diffusion3d_fused_variant_ok", &diffusion3d_fused_variant_ok);
   m.def("diffusion3d_variant_compiled", &stencil_variant_compiled,
         "Whether stencil variant v is compiled in this build (measurement-only ones: build.py --probes).");
@@ -688,15 +689,15 @@ PYBIND11_MODULE(_igg_native, m) {
       .def("step",
            [](FusedHalo& f, uintptr_t t2, uintptr_t t, uintptr_t cp, const std::array<double, 3>& rd2,
               double dtlam, int variant, int64_t step, bool primed, uintptr_t stream, int rounds, int mode,
-              bool entry) {
+              bool entry, bool halo_z) {
              TraceRange tr("igg.diffusion3d_fused");
-             DiffusionArgs a{t2, t, cp, {0, 0, 0}, {rd2[0], rd2[1], rd2[2]}, dtlam, 0, rounds};
+             DiffusionArgs a{t2, t, cp, {0, 0, 0}, {rd2[0], rd2[1], rd2[2]}, dtlam, 0, rounds, halo_z};
              f.step_shape(a);
              f.step(a, variant, mode, step, primed, as_stream(stream), entry);
            },
            py::arg("t2"), py::arg("t"), py::arg("cp"), py::arg("rd2"), py::arg("dtlam"), py::arg("variant"),
            py::arg("step"), py::arg("primed"), py::arg("stream"), py::arg("rounds") = 0, py::arg("mode") = 0,
-           py::arg("entry") = false)
+           py::arg("entry") = false, py::arg("halo_z") = false)
       .def("sync", [](FusedHalo& f, uintptr_t s) { f.sync(as_stream(s)); })
       .def("drain", [](FusedHalo& f, uintptr_t s) { f.drain(as_stream(s)); }, py::arg("stream"),
            "Exit barrier after in-kernel synchronised steps (collective; no-op after a sync-kernel step).")

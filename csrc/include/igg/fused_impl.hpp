@@ -91,6 +91,10 @@ struct HxScal {
   // tz_hi) exchanges.
   int order, order_lo, order_hi;
   int64_t tz_hi;
+  // DiffusionArgs::halo_z per z side: the z-edge lane stores its whole vector
+  // (t's value in t2's halo element) - only on a side without a z neighbour
+  // (with one, the neighbour's direct-z stores or sync_halo own that element).
+  int zh_lo, zh_hi;
   StepSync sync;  // in-kernel step synchronisation (put.hpp; my_flags null: a sync kernel follows)
 };
 
@@ -205,6 +209,7 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   // Lanes past the box alias the last valid vector (zc < z0) and compute
   // garbage there: they must not store (remote whole-vector stores included).
   const bool zown = zc == z0;
+  const bool zfull = zown && ((z0 == 0 && a.zh_lo) || (z0 + VZ == n2 && a.zh_hi));
   const bool load_prev = lane == 0;
   const bool load_next = lane == 63 || z0 + VZ > zhi_v;
   const int zpi = static_cast<int>(max<int64_t>(zc - 1, 0) - zt);
@@ -456,6 +461,14 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
           else
 #endif
           __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
+        } else if (zfull) {
+          // a z-edge lane (halo_z): the whole vector with t's value in the
+          // halo element, one full-line store instead of a partial line
+          V o = out;
+#pragma unroll
+          for (int e = 0; e < VZ; ++e)
+            if (z0 + e == 0 || z0 + e == hi2) o[e] = c[e];
+          __builtin_nontemporal_store(o, reinterpret_cast<V*>(dst));
         } else {
 #pragma unroll
           for (int e = 0; e < VZ; ++e)
@@ -710,6 +723,8 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   a.order_lo = (FZ_ != 0 && (io.in[2][0] || io.out[2][0])) ? 1 : 0;
   a.order_hi = (FZ_ != 0 && (io.in[2][1] || io.out[2][1])) ? 1 : 0;
   a.tz_hi = (n2 - VZ) / W;
+  a.zh_lo = (d.halo_z && !io.in[2][0] && !io.out[2][0]) ? 1 : 0;
+  a.zh_hi = (d.halo_z && !io.in[2][1] && !io.out[2][1]) ? 1 : 0;
   a.sync = StepSync{};
   // In-kernel step sync: the specialised kernel only (per-wave feature
   // classes), and not under the diagnostics that override the classes.

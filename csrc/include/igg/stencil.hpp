@@ -33,6 +33,15 @@ struct DiffusionArgs {
   int elem_bytes;           // 8 (f64) or 4 (f32)
   int rounds = 0;           // grid sizing for this launch: 0 = global default,
                             // k > 0 = k residency rounds, k < 0 = |k|*4096 blocks
+  // Z-edge stores of the inner box: false = only [1, n-1) is written (the
+  // z-edge lanes store 1 or 3 elements, i.e. part of a cache line); true = those
+  // lanes store their whole vector, writing t's value into t2's halo element
+  // (z = 0 / n2-1) - a full-line store. Only where that is a no-op or is
+  // overwritten later: t2's z halo equals t's (fixed boundaries, T2 = T.clone())
+  // or the halo update that follows the stencil rewrites it, and nothing writes
+  // t2's z halo concurrently. 1024^3 f32: -5.5..-6.8 % per step, 512^3 f64:
+  // up to -2.9 % (profiles/r4_halo_z/).
+  bool halo_z = false;
 };
 
 // Number of tuned kernel variants (see stencil_kernels.hip); variant 0 = default.

@@ -42,6 +42,7 @@ struct KArgs {
   const T* __restrict__ cp;
   int64_t n0, n1, n2;
   T rdx2, rdy2, rdz2, dtlam;
+  int halo_z;  // DiffusionArgs::halo_z: z-edge lanes store whole vectors (halo elements copied from t)
 };
 
 __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
@@ -181,6 +182,7 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
   const int64_t zc = min(max(z0, zlo_v), zhi_v);
   const int zl = static_cast<int>(zc - zt);                  // per-lane offset in the tile
   const bool lane_full = z0 >= lo2 && z0 + VZ <= hi2;
+  const bool zfull = a.halo_z && lo2 == 1 && hi2 == n2 - 1 && zc == z0 && z0 + VZ <= n2;
   // z-neighbours come from lane neighbours except where that neighbour lane is
   // clamped (or outside the wave): those lanes load their edge value directly.
   const bool load_prev = lane == 0 || z0 - VZ < zlo_v;
@@ -247,6 +249,16 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
         if (lane_full) {
           if (NT) __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
           else *reinterpret_cast<V*>(dst) = out;
+        } else if (zfull) {
+          // the z-edge lane of a full-z box: the halo element (z = 0 or n2-1)
+          // is written with t's value, so the whole vector - and its cache
+          // line - is stored instead of a partial line
+          V o = out;
+#pragma unroll
+          for (int e = 0; e < VZ; ++e)
+            if (z0 + e < lo2 || z0 + e >= hi2) o[e] = c[e];
+          if (NT) __builtin_nontemporal_store(o, reinterpret_cast<V*>(dst));
+          else *reinterpret_cast<V*>(dst) = o;
         } else {
 #pragma unroll
           for (int e = 0; e < VZ; ++e)
@@ -478,6 +490,7 @@ KArgs<T> make_args(const DiffusionArgs& a) {
   k.rdy2 = static_cast<T>(a.rd2[1]);
   k.rdz2 = static_cast<T>(a.rd2[2]);
   k.dtlam = static_cast<T>(a.dt_lam);
+  k.halo_z = a.halo_z ? 1 : 0;
   return k;
 }
 

@@ -31,6 +31,7 @@ bitwise identical to the update_halo_ path.
 from __future__ import annotations
 
 import math
+import os
 import warnings
 
 import torch
@@ -47,6 +48,13 @@ from ..utils.tools import coords_g, nx_g, ny_g, nz_g
 GRAPH_STEPS = 10
 # Candidates re-timed by the autotune's ping-pong stage (_choose_variant).
 PINGPONG_FRONT = 4
+# Whole-line z-edge stores of the full-box steps (ops.stencil.diffusion3d_
+# halo_z; the fused step on its z sides without a neighbour): T2's z halo gets
+# T's values, which is a no-op at fixed boundaries (T2 = T.clone() at init,
+# neither is ever changed there) and is rewritten by the exchange elsewhere.
+# 1024^3 f32 -5.5..-6.8 %, 512^3 f64 up to -2.9 % per variant
+# (profiles/r4_halo_z/). IGG_HALO_Z=0 restores partial-line edge stores.
+HALO_Z = os.environ.get("IGG_HALO_Z", "1").strip() != "0"
 
 
 def _rccl_transport() -> bool:
@@ -344,11 +352,11 @@ class Diffusion3D:
                 with self.timer.phase("stencil+exchange"):
                     self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
                                   self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
-                                  mode, self._fentry)
+                                  mode, self._fentry, HALO_Z)
             else:
                 self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
                               self.fused_variant, self._fstep, self._fprimed, s, self.fused_rounds,
-                              mode, self._fentry)
+                              mode, self._fentry, HALO_Z)
             self._fentry = False
             self._fstep += 1
             self._fprimed = True
@@ -397,11 +405,14 @@ class Diffusion3D:
                     main.wait_stream(cs)
         elif self.timer is not None:
             with self.timer.phase("stencil"):
-                stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
+                stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, halo_z=HALO_Z, **self._kw())
             with self.timer.phase("update_halo"):
                 update_halo_(T2)
         else:
-            stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, **self._kw())
+            # halo_z: T2's z halo gets T's values (whole-line z-edge stores):
+            # at a physical boundary both hold the same fixed values, and
+            # update_halo_(T2) right after rewrites every exchanged one
+            stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, halo_z=HALO_Z, **self._kw())
             update_halo_(T2)
         self.T, self.T2 = T2, T
         self._warm = True
@@ -571,7 +582,7 @@ def _choose_variant(m: "Diffusion3D") -> int:
 
     # Stage 1: every (variant, rounds) on fixed buffers (T2 = f(T), cheap).
     t = stencil.time_variants(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes,
-                              [(v, r) for v in stencil.SHORTLIST for r in stencil.GRID_ROUNDS])
+                              [(v, r) for v in stencil.SHORTLIST for r in stencil.GRID_ROUNDS], halo_z=HALO_Z)
     cands, tot = summed(t)
     m.variant_times = {f"{v}@r{r}": round(float(x) / max(1, int(gg.nprocs)), 5) for (v, r), x in zip(cands, tot)}
     # Stage 2: the stage-1 front again, in the time loop's ping-pong shape and
@@ -579,7 +590,7 @@ def _choose_variant(m: "Diffusion3D") -> int:
     # biased low and the alternating buffers cost ~1 % (profiles/r2_gap/), so
     # the pick is made on what the run actually does.
     front = [cands[i] for i in torch.argsort(tot)[:PINGPONG_FRONT].tolist()]
-    t2 = stencil.time_variants_pingpong(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes, front)
+    t2 = stencil.time_variants_pingpong(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes, front, halo_z=HALO_Z)
     cands2, tot2 = summed(t2)
     m.variant_times.update({f"{v}@r{r}/pp": round(float(x) / max(1, int(gg.nprocs)), 5)
                             for (v, r), x in zip(cands2, tot2)})

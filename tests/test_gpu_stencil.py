@@ -148,3 +148,37 @@ def test_autotune_pingpong_stage(gpu):
         assert torch.equal(m.T, ref.T)  # variants are bitwise interchangeable
     finally:
         igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.parametrize("variant", stencil.compiled_variants())
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_halo_z_whole_line_edges(gpu, variant, dtype):
+    """halo_z=True: the full inner box computes the same interior bitwise, and
+    the only other cells written are T2's z halo elements (z = 0, nz-1) of the
+    inner rows, which get T's values; a box that does not span the whole inner
+    z range writes nothing outside itself."""
+    for shape in [(24, 20, 72), (9, 70, 16), (20, 22, 132)]:
+        T, Cp, Tg, Cpg = _fields(shape, dtype, gpu)
+        a = torch.full(shape, -7.0, dtype=dtype, device=gpu)
+        b = a.clone()
+        stencil.diffusion3d_(a, Tg, Cpg, variant=variant, **KW)
+        stencil.diffusion3d_(b, Tg, Cpg, variant=variant, halo_z=True, **KW)
+        torch.cuda.synchronize()
+        n0, n1, n2 = shape
+        inner = (slice(1, n0 - 1), slice(1, n1 - 1))
+        assert torch.equal(a[1:-1, 1:-1, 1:-1], b[1:-1, 1:-1, 1:-1]), shape
+        want = a.clone()
+        want[inner + (0,)] = Tg[inner + (0,)]
+        want[inner + (n2 - 1,)] = Tg[inner + (n2 - 1,)]
+        # vector kernels write whole edge vectors; the scalar fallbacks (and
+        # shapes the vector path cannot take) leave the halo untouched
+        same_as_plain = torch.equal(b, a)
+        assert same_as_plain or torch.equal(b, want), (shape, variant)
+        c = torch.full(shape, -7.0, dtype=dtype, device=gpu)
+        box = [([1, 1, 2], [n0 - 1, n1 - 1, n2 - 1])]
+        stencil.diffusion3d_(c, Tg, Cpg, variant=variant, boxes=box, halo_z=True, **KW)
+        torch.cuda.synchronize()
+        mask = torch.zeros(shape, dtype=torch.bool, device=gpu)
+        mask[1:-1, 1:-1, 2:-1] = True
+        assert (c[~mask] == -7.0).all(), (shape, variant)
+        assert torch.equal(c[mask], a[mask]), (shape, variant)
