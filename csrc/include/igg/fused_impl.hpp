@@ -92,8 +92,8 @@ struct HxScal {
   int order, order_lo, order_hi;
   int64_t tz_hi;
   // DiffusionArgs::halo_z per z side: the z-edge lane stores its whole vector
-  // (t's value in t2's halo element) - only on a side without a z neighbour
-  // (with one, the neighbour's direct-z stores or sync_halo own that element).
+  // (its halo element - t's value, or the received one - into t2's halo) as
+  // one full-line store (launch_hx decides per side).
   int zh_lo, zh_hi;
   StepSync sync;  // in-kernel step synchronisation (put.hpp; my_flags null: a sync kernel follows)
 };
@@ -723,8 +723,13 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   a.order_lo = (FZ_ != 0 && (io.in[2][0] || io.out[2][0])) ? 1 : 0;
   a.order_hi = (FZ_ != 0 && (io.in[2][1] || io.out[2][1])) ? 1 : 0;
   a.tz_hi = (n2 - VZ) / W;
-  a.zh_lo = (d.halo_z && !io.in[2][0] && !io.out[2][0]) ? 1 : 0;
-  a.zh_hi = (d.halo_z && !io.in[2][1] && !io.out[2][1]) ? 1 : 0;
+  // halo_z per z side: without a neighbour (fixed boundary: T2's halo equals
+  // T's), or with the arena z exchange (the edge lane holds the received halo
+  // value: T2's halo planes are stale by design in fused mode and rewritten by
+  // sync_halo; nobody else writes them). Not with direct z: the neighbour
+  // stores into exactly that element while this kernel runs.
+  a.zh_lo = (d.halo_z && (io.in[2][0] || !io.out[2][0])) ? 1 : 0;
+  a.zh_hi = (d.halo_z && (io.in[2][1] || !io.out[2][1])) ? 1 : 0;
   a.sync = StepSync{};
   // In-kernel step sync: the specialised kernel only (per-wave feature
   // classes), and not under the diagnostics that override the classes.
