@@ -74,12 +74,20 @@ def build(jobs: int | None = None, debug: bool = False, asan: bool = False, verb
     BUILD.mkdir(parents=True, exist_ok=True)
     flags = ["-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-result"]
     flags += ["-O0", "-g"] if debug else ["-O3"]
+    # No floating-point contraction: the stencil variants, the fused exchange
+    # forms and the plain steps must compute bitwise the same values (the
+    # bench's checks and tests compare them exactly), and with contraction on
+    # the compiler fuses a*b+c into an FMA per instantiation as register
+    # pressure and scheduling dictate - one changed fused form differed from
+    # the plain step by 1 ulp at 2 cells (round 4, f32 tiling 40 direct z).
+    # Formulas that want an FMA spell it out (__builtin_fma).
+    flags += ["-ffp-contract=off"]
     if asan:
         # Host-code sanitizer only (GPU ASan is not available on the pool).
         flags += ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
     if probes:
         flags += ["-DIGG_PROBES"]
-    tag = ("dbg" if debug else "opt") + ("-asan" if asan else "") + ("-probes" if probes else "")
+    tag = ("dbg" if debug else "opt") + ("-asan" if asan else "") + ("-probes" if probes else "") + "-fpc0"
     hdr_t = _headers_mtime()
     todo = []
     objs = []

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "igg/devmath.hpp"
 #include "igg/devsync.hpp"
 #include "igg/stencil.hpp"
 #include "igg/sysstore.hpp"
@@ -449,7 +450,7 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         const T xpv = RV ? tm[r][e] : tp[r][e], xmv = RV ? tp[r][e] : tm[r][e];  // planes x+1, x-1
         const T lap = (xpv - c2 + xmv) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
                       (zp - c2 + zm) * a.rdz2;
-        out[e] = c[e] + a.dtlam / cp[r][e] * lap;
+        out[e] = fmad(a.dtlam / cp[r][e], lap, c[e]);
       }
       if (r < nv) {
         T* dst = t2 + off + rowb[r] + zl;

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 
+#include "igg/devmath.hpp"
 #include "igg/stencil.hpp"
 
 namespace igg {
@@ -118,7 +119,7 @@ diffusion3d_kernel(const KArgs<T> a, const BoxTable bt) {
       const T c2 = two * tc[r];
       const T lap = (tp[r] - c2 + tm[r]) * a.rdx2 + (ynext - c2 + yprev) * a.rdy2 +
                     (zp[r] - c2 + zm[r]) * a.rdz2;
-      const T out = tc[r] + a.dtlam / cp[r] * lap;
+      const T out = fmad(a.dtlam / cp[r], lap, tc[r]);
       if (valid[r]) a.t2[off + row[r]] = out;
     }
 #pragma unroll
@@ -242,7 +243,7 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
         const T c2 = two * c[e];
         const T lap = (tp[r][e] - c2 + tm[r][e]) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
                       (zp - c2 + zm) * a.rdz2;
-        out[e] = c[e] + a.dtlam / cp[r][e] * lap;
+        out[e] = fmad(a.dtlam / cp[r][e], lap, c[e]);
       }
       if (r < nv) {
         T* dst = a.t2 + off + rowb[r] + zl;
