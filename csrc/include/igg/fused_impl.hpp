@@ -323,7 +323,6 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
     tp[r] = vld<T, VZ>(plane(xf + DX) + rowb[r] + zl);
     cp[r] = ldc(cpp + xf * s0 + rowb[r] + zl);
   }
-  const T two = T(2);
   T evn = T(0);
   if constexpr ((FEAT & 512) != 0 && (FEAT & 16384) == 0) evn = t[xf * s0 + rowe];
   int64_t x = xf;
@@ -446,11 +445,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
       for (int e = 0; e < VZ; ++e) {
         const T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
         const T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
-        const T c2 = two * c[e];
         const T xpv = RV ? tm[r][e] : tp[r][e], xmv = RV ? tp[r][e] : tm[r][e];  // planes x+1, x-1
-        const T lap = (xpv - c2 + xmv) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
-                      (zp - c2 + zm) * a.rdz2;
-        out[e] = fmad(a.dtlam / cp[r][e], lap, c[e]);
+        out[e] = diffusion_point(c[e], xmv, xpv, yv[e], yn[e], zm, zp, cp[r][e], a.rdx2, a.rdy2, a.rdz2, a.dtlam);
       }
       if (r < nv) {
         T* dst = t2 + off + rowb[r] + zl;

@@ -99,7 +99,6 @@ diffusion3d_kernel(const KArgs<T> a, const BoxTable bt) {
     tm[r] = t[(xs - 1) * s0 + row[r]];
     tc[r] = t[xs * s0 + row[r]];
   }
-  const T two = T(2);
   for (int64_t x = xs; x < xe; ++x) {
     const int64_t off = x * s0;
     T tp[RY], zm[RY], zp[RY], cp[RY];
@@ -116,10 +115,8 @@ diffusion3d_kernel(const KArgs<T> a, const BoxTable bt) {
     for (int r = 0; r < RY; ++r) {
       const T yprev = (r == 0) ? ym : tc[r - 1];
       const T ynext = (r + 1 < nv) ? tc[(r + 1 < RY) ? r + 1 : r] : yp;
-      const T c2 = two * tc[r];
-      const T lap = (tp[r] - c2 + tm[r]) * a.rdx2 + (ynext - c2 + yprev) * a.rdy2 +
-                    (zp[r] - c2 + zm[r]) * a.rdz2;
-      const T out = fmad(a.dtlam / cp[r], lap, tc[r]);
+      const T out = diffusion_point(tc[r], tm[r], tp[r], yprev, ynext, zm[r], zp[r], cp[r], a.rdx2, a.rdy2, a.rdz2,
+                                    a.dtlam);
       if (valid[r]) a.t2[off + row[r]] = out;
     }
 #pragma unroll
@@ -206,7 +203,6 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
     tp[r] = vload<T, VZ>(t + (xs + 1) * s0 + rowb[r] + zl);
     cp[r] = vload<T, VZ>(cpp + xs * s0 + rowb[r] + zl);
   }
-  const T two = T(2);
   for (int64_t x = xs; x < xe; ++x) {
     const int64_t off = x * s0;
     V tn[RY], cpn[RY];
@@ -240,10 +236,8 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
       for (int e = 0; e < VZ; ++e) {
         const T zm = e == 0 ? prev : c[e > 0 ? e - 1 : 0];
         const T zp = e == VZ - 1 ? next : c[e + 1 < VZ ? e + 1 : e];
-        const T c2 = two * c[e];
-        const T lap = (tp[r][e] - c2 + tm[r][e]) * a.rdx2 + (yn[e] - c2 + yv[e]) * a.rdy2 +
-                      (zp - c2 + zm) * a.rdz2;
-        out[e] = fmad(a.dtlam / cp[r][e], lap, c[e]);
+        out[e] = diffusion_point(c[e], tm[r][e], tp[r][e], yv[e], yn[e], zm, zp, cp[r][e], a.rdx2, a.rdy2, a.rdz2,
+                                 a.dtlam);
       }
       if (r < nv) {
         T* dst = a.t2 + off + rowb[r] + zl;
