@@ -149,9 +149,12 @@ __device__ __forceinline__ HxTile<T> hx_tile(const HxScal<T>& a, int64_t bid, in
 // 64 x-out, 128 y-out; 256 = non-temporal Cp loads (plain variants); 512 =
 // lane-distributed z-segment edge loads (plain variants, below); 1024 = one
 // workgroup per CU (launch); 2048 = no per-wave specialisation (kernel below);
-// 4096 = z edge values staged through LDS instead of v_readlane. 207 = the full
+// 4096 = z edge values staged through LDS instead of v_readlane; HZ (262144) =
+// the whole-line z-edge store form (DiffusionArgs::halo_z). 207 = the full
 // exchange, 0 = the plain update (variants 21+); other subsets served the cost
 // bisect (profiles/r1_fused/feature_bisect_*).
+constexpr int HZ = 262144;
+
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT>
 __device__ __forceinline__ void
 hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
@@ -210,7 +213,7 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   // Lanes past the box alias the last valid vector (zc < z0) and compute
   // garbage there: they must not store (remote whole-vector stores included).
   const bool zown = zc == z0;
-  const bool zfull = zown && ((z0 == 0 && a.zh_lo) || (z0 + VZ == n2 && a.zh_hi));
+  const bool zfull = (FEAT & HZ) != 0 && zown && ((z0 == 0 && a.zh_lo) || (z0 + VZ == n2 && a.zh_hi));
   const bool load_prev = lane == 0;
   const bool load_next = lane == 63 || z0 + VZ > zhi_v;
   const int zpi = static_cast<int>(max<int64_t>(zc - 1, 0) - zt);
@@ -458,7 +461,7 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
           else
 #endif
           __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
-        } else if (zfull) {
+        } else if ((FEAT & HZ) != 0 && zfull) {
           // a z-edge lane (halo_z): the whole vector with t's value in the
           // halo element, one full-line store instead of a partial line
           V o = out;

@@ -19,13 +19,16 @@ template <typename T>
 void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
   const HaloIOArgs none{};
   switch (v) {  // tilings of the shortlisted restrict-form variants 21/23/24/25/26/40/43
-    case 0: launch_hx<T, 4, 4, 4, false, 1, false, 0>(d, none, s); break;
-    case 9: launch_hx<T, 4, 8, 4, false, 1, false, 0>(d, none, s); break;
-    case 11: launch_hx<T, 4, 8, 2, false, 1, false, 0>(d, none, s); break;
-    case 14: launch_hx<T, 2, 8, 4, false, 2, false, 0>(d, none, s); break;
-    case 100: launch_hx<T, 2, 8, 2, false, 1, false, 0>(d, none, s); break;
-    case 124: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024>(d, none, s); break;
-    case 141: launch_hx<T, 2, 8, 2, false, 4, false, 0>(d, none, s); break;
+    // HZ: the whole-line z-edge store form (DiffusionArgs::halo_z decides at
+    // run time); compiled into the plain sweeps only - the fused kernels sit at
+    // the VGPR limit and the extra code slowed them (profiles/r4_halo_z/)
+    case 0: launch_hx<T, 4, 4, 4, false, 1, false, HZ>(d, none, s); break;
+    case 9: launch_hx<T, 4, 8, 4, false, 1, false, HZ>(d, none, s); break;
+    case 11: launch_hx<T, 4, 8, 2, false, 1, false, HZ>(d, none, s); break;
+    case 14: launch_hx<T, 2, 8, 4, false, 2, false, HZ>(d, none, s); break;
+    case 100: launch_hx<T, 2, 8, 2, false, 1, false, HZ>(d, none, s); break;
+    case 124: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | HZ>(d, none, s); break;
+    case 141: launch_hx<T, 2, 8, 2, false, 4, false, HZ>(d, none, s); break;
 #ifdef IGG_PROBES
     // measured and not adopted (rounds 1-2): other tilings, non-temporal Cp,
     // lane-distributed z edges of other tilings, full-row z tiles, and the
