@@ -1286,6 +1286,7 @@ def main():
                                   else {"acoustic": "fused staggered faces"})
                                  if getattr(model, "fused", False) else None),
                 "stencil_grid_rounds": getattr(model, "rounds", None),
+                "stencil_halo_z": getattr(model, "halo_z", None),
                 "fused_ab_ms": fused_ab,
                 "stencil_variant": getattr(model, "variant", None),
                 "stencil_variant_ms": getattr(model, "variant_times", None),

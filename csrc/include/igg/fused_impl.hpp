@@ -251,6 +251,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   const bool zin_lo = (FEAT & 4) && has_lo && zi0, zin_hi = (FEAT & 4) && has_hi && zi1;
   const bool zout_lo = (FEAT & 8) && has_lo && zo0, zout_hi = (FEAT & 8) && has_hi && zo1;
   const bool zin = zin_lo || zin_hi, zout = zout_lo || zout_hi;
+  // halo_z (FEAT HZ): this wave holds a z edge whose halo element it may write
+  const bool hz_wave = (FEAT & HZ) != 0 && ((has_lo && a.zh_lo) || (has_hi && a.zh_hi));
   const int rl = lane & 31;
   // Lane-distributed z values: row r of the low edge in lane r, of the high
   // edge in lane 32+r (rows < nv).
@@ -453,7 +455,18 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
       }
       if (r < nv) {
         T* dst = t2 + off + rowb[r] + zl;
-        if (lane_full) {
+        if constexpr ((FEAT & HZ) != 0) {
+          // a z-edge lane (halo_z): its halo element takes t's value (or the
+          // received one), in place, so the whole vector - one full line - is
+          // stored below instead of a partial line; a wave-uniform branch, so
+          // waves away from the z edges run none of it
+          if (hz_wave && zfull) {
+#pragma unroll
+            for (int e = 0; e < VZ; ++e)
+              if (z0 + e == 0 || z0 + e == hi2) out[e] = c[e];
+          }
+        }
+        if (lane_full || ((FEAT & HZ) != 0 && zfull)) {
 #ifdef IGG_PROBES
           // FEAT 131072: plain (temporal) stores, to measure what the
           // non-temporal hint costs or saves in the Infinity Cache
@@ -461,14 +474,6 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
           else
 #endif
           __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
-        } else if ((FEAT & HZ) != 0 && zfull) {
-          // a z-edge lane (halo_z): the whole vector with t's value in the
-          // halo element, one full-line store instead of a partial line
-          V o = out;
-#pragma unroll
-          for (int e = 0; e < VZ; ++e)
-            if (z0 + e == 0 || z0 + e == hi2) o[e] = c[e];
-          __builtin_nontemporal_store(o, reinterpret_cast<V*>(dst));
         } else {
 #pragma unroll
           for (int e = 0; e < VZ; ++e)
@@ -795,16 +800,16 @@ void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStre
     // receivers' field halo elements, so the z-edge waves read their halo
     // from the field like every other wave and carry only the send code.
     if (io.in[2][0] || io.in[2][1]) fail("diffusion3d (fused halo): direct z mode with z arena input");
-    if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF>(d, io, s, pk, ord);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF>(d, io, s, pk, ord);
+    if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF | HZ>(d, io, s, pk, ord);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF | HZ>(d, io, s, pk, ord);
   } else if (zx || !(mode & 2)) {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF>(d, io, s, pk, ord);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF>(d, io, s, pk, ord);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 207 | XF | HZ>(d, io, s, pk, ord);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 207 | XF | HZ>(d, io, s, pk, ord);
   } else {
     mode &= 1;
-    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF>(d, io, s, pk, ord);
-    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF>(d, io, s, pk, ord);
+    if (mode == 0) launch_hx<T, BY, RY, VZ, PF, BZ, false, 195 | XF | HZ>(d, io, s, pk, ord);
+    else launch_hx<T, BY, RY, VZ, PF, BZ, true, 195 | XF | HZ>(d, io, s, pk, ord);
   }
 }
 

@@ -19,16 +19,19 @@ template <typename T>
 void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
   const HaloIOArgs none{};
   switch (v) {  // tilings of the shortlisted restrict-form variants 21/23/24/25/26/40/43
-    // HZ: the whole-line z-edge store form (DiffusionArgs::halo_z decides at
-    // run time); compiled into the plain sweeps only - the fused kernels sit at
-    // the VGPR limit and the extra code slowed them (profiles/r4_halo_z/)
-    case 0: launch_hx<T, 4, 4, 4, false, 1, false, HZ>(d, none, s); break;
-    case 9: launch_hx<T, 4, 8, 4, false, 1, false, HZ>(d, none, s); break;
-    case 11: launch_hx<T, 4, 8, 2, false, 1, false, HZ>(d, none, s); break;
-    case 14: launch_hx<T, 2, 8, 4, false, 2, false, HZ>(d, none, s); break;
-    case 100: launch_hx<T, 2, 8, 2, false, 1, false, HZ>(d, none, s); break;
-    case 124: launch_hx<T, 4, 8, 2, false, 1, false, 512 | 1024 | HZ>(d, none, s); break;
-    case 141: launch_hx<T, 2, 8, 2, false, 4, false, HZ>(d, none, s); break;
+    // each tiling in the partial-line and the whole-line (HZ, halo_z) z-edge
+    // store form: the autotune times both (models/diffusion3d.py)
+#define IGG_PLAIN_HX(BY, RY, VZ, BZ, F)                                         \
+  (d.halo_z ? launch_hx<T, BY, RY, VZ, false, BZ, false, (F) | HZ>(d, none, s) \
+            : launch_hx<T, BY, RY, VZ, false, BZ, false, (F)>(d, none, s))
+    case 0: IGG_PLAIN_HX(4, 4, 4, 1, 0); break;
+    case 9: IGG_PLAIN_HX(4, 8, 4, 1, 0); break;
+    case 11: IGG_PLAIN_HX(4, 8, 2, 1, 0); break;
+    case 14: IGG_PLAIN_HX(2, 8, 4, 2, 0); break;
+    case 100: IGG_PLAIN_HX(2, 8, 2, 1, 0); break;
+    case 124: IGG_PLAIN_HX(4, 8, 2, 1, 512 | 1024); break;
+    case 141: IGG_PLAIN_HX(2, 8, 2, 4, 0); break;
+#undef IGG_PLAIN_HX
 #ifdef IGG_PROBES
     // measured and not adopted (rounds 1-2): other tilings, non-temporal Cp,
     // lane-distributed z edges of other tilings, full-row z tiles, and the

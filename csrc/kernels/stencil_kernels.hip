@@ -146,7 +146,10 @@ __device__ __forceinline__ typename VecOf<T, VZ>::type vload(const T* p) {
   return *reinterpret_cast<const typename VecOf<T, VZ>::type*>(p);
 }
 
-template <typename T, int BY, int RY, int VZ, bool PF, bool NT, int BZ>
+// HZ: the whole-line z-edge store form (DiffusionArgs::halo_z), a separate
+// instantiation - its extra branches cost tiling 11 2.7 % where the partial
+// edge stores cost it nothing, so the autotune times both forms.
+template <typename T, int BY, int RY, int VZ, bool PF, bool NT, int BZ, bool HZ>
 __global__ void __launch_bounds__(64 * BY * BZ)
 diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
   using V = typename VecOf<T, VZ>::type;
@@ -180,7 +183,7 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
   const int64_t zc = min(max(z0, zlo_v), zhi_v);
   const int zl = static_cast<int>(zc - zt);                  // per-lane offset in the tile
   const bool lane_full = z0 >= lo2 && z0 + VZ <= hi2;
-  const bool zfull = a.halo_z && lo2 == 1 && hi2 == n2 - 1 && zc == z0 && z0 + VZ <= n2;
+  const bool zfull = HZ && lo2 == 1 && hi2 == n2 - 1 && zc == z0 && z0 + VZ <= n2;
   // z-neighbours come from lane neighbours except where that neighbour lane is
   // clamped (or outside the wave): those lanes load their edge value directly.
   const bool load_prev = lane == 0 || z0 - VZ < zlo_v;
@@ -244,7 +247,7 @@ diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
         if (lane_full) {
           if (NT) __builtin_nontemporal_store(out, reinterpret_cast<V*>(dst));
           else *reinterpret_cast<V*>(dst) = out;
-        } else if (zfull) {
+        } else if (HZ && zfull) {
           // the z-edge lane of a full-z box: the halo element (z = 0 or n2-1)
           // is written with t's value, so the whole vector - and its cache
           // line - is stored instead of a partial line
@@ -429,18 +432,27 @@ void launch_scalar(const KArgs<T>& ka, const std::vector<Box>& boxes, hipStream_
   });
 }
 
+template <typename T, int BY, int RY, int VZ, bool PF, bool NT, int BZ, bool HZ>
+void launch_vector_form(const KArgs<T>& ka, const std::vector<Box>& boxes, hipStream_t stream) {
+  const void* kern = reinterpret_cast<const void*>(&diffusion3d_vkernel<T, BY, RY, VZ, PF, NT, BZ, HZ>);
+  for_each_table(boxes, 64 * VZ * BZ, BY * RY, true, target_for(kern, 64 * BY * BZ), [&](const BoxTable& bt, unsigned blocks) {
+    hipLaunchKernelGGL((diffusion3d_vkernel<T, BY, RY, VZ, PF, NT, BZ, HZ>), dim3(blocks), dim3(64 * BY * BZ), 0,
+                       stream, ka, bt);
+    IGG_HIP_CHECK(hipGetLastError());
+  });
+}
+
 template <typename T, int BY, int RY, int VZ, bool PF, bool NT, int BZ = 1>
 void launch_vector(const KArgs<T>& ka, const std::vector<Box>& boxes, hipStream_t stream) {
   if (ka.n2 % VZ != 0 || ka.n2 < 2 * VZ) {  // vector path needs aligned rows
     launch_scalar<T, 4, 8, true>(ka, boxes, stream);
     return;
   }
-  const void* kern = reinterpret_cast<const void*>(&diffusion3d_vkernel<T, BY, RY, VZ, PF, NT, BZ>);
-  for_each_table(boxes, 64 * VZ * BZ, BY * RY, true, target_for(kern, 64 * BY * BZ), [&](const BoxTable& bt, unsigned blocks) {
-    hipLaunchKernelGGL((diffusion3d_vkernel<T, BY, RY, VZ, PF, NT, BZ>), dim3(blocks), dim3(64 * BY * BZ), 0,
-                       stream, ka, bt);
-    IGG_HIP_CHECK(hipGetLastError());
-  });
+  if (ka.halo_z) {
+    launch_vector_form<T, BY, RY, VZ, PF, NT, BZ, true>(ka, boxes, stream);
+  } else {
+    launch_vector_form<T, BY, RY, VZ, PF, NT, BZ, false>(ka, boxes, stream);
+  }
 }
 
 template <typename T>

@@ -88,6 +88,7 @@ class Diffusion3D:
         self.dt = min(self.dx ** 2, self.dy ** 2, self.dz ** 2) * cp_min / lam / 8.1
         self.variant = variant
         self.rounds = 0  # grid residency rounds of the full-interior launch (0: library default)
+        self.halo_z = HALO_Z  # whole-line z-edge stores of the full-interior launch (autotuned per variant)
         self.variant_times = None  # per-variant ms when autotuned (see _choose_variant)
         self.timer = None  # optional utils.trace.PhaseTimer (eager steps only)
         # Overlap tuning knobs: kernel variant / grid rounds of the boundary
@@ -405,14 +406,14 @@ class Diffusion3D:
                     main.wait_stream(cs)
         elif self.timer is not None:
             with self.timer.phase("stencil"):
-                stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, halo_z=HALO_Z, **self._kw())
+                stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, halo_z=self.halo_z, **self._kw())
             with self.timer.phase("update_halo"):
                 update_halo_(T2)
         else:
             # halo_z: T2's z halo gets T's values (whole-line z-edge stores):
             # at a physical boundary both hold the same fixed values, and
             # update_halo_(T2) right after rewrites every exchanged one
-            stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, halo_z=HALO_Z, **self._kw())
+            stencil.diffusion3d_(T2, T, Cp, boxes=self.inner, halo_z=self.halo_z, **self._kw())
             update_halo_(T2)
         self.T, self.T2 = T2, T
         self._warm = True
@@ -580,22 +581,30 @@ def _choose_variant(m: "Diffusion3D") -> int:
             dist.all_reduce(tot, group=gg.comm.gloo)
         return cands, tot
 
-    # Stage 1: every (variant, rounds) on fixed buffers (T2 = f(T), cheap).
+    # Stage 1: every (variant, rounds, z-edge store form) on fixed buffers
+    # (T2 = f(T), cheap). The whole-line form (halo_z) wins for most tilings
+    # and costs tiling 11 2.7 % (profiles/r4_halo_z/), so both are timed.
+    forms = (True, False) if HALO_Z else (False,)
     t = stencil.time_variants(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes,
-                              [(v, r) for v in stencil.SHORTLIST for r in stencil.GRID_ROUNDS], halo_z=HALO_Z)
+                              [(v, r, hz) for v in stencil.SHORTLIST for r in stencil.GRID_ROUNDS for hz in forms])
     cands, tot = summed(t)
-    m.variant_times = {f"{v}@r{r}": round(float(x) / max(1, int(gg.nprocs)), 5) for (v, r), x in zip(cands, tot)}
+
+    def key(v, r, hz):
+        return f"{v}@r{r}" + ("/hz" if hz else "")
+
+    m.variant_times = {key(*c): round(float(x) / max(1, int(gg.nprocs)), 5) for c, x in zip(cands, tot)}
     # Stage 2: the stage-1 front again, in the time loop's ping-pong shape and
     # with more launches: the minimum over ~44 noisy fixed-buffer timings is
     # biased low and the alternating buffers cost ~1 % (profiles/r2_gap/), so
     # the pick is made on what the run actually does.
     front = [cands[i] for i in torch.argsort(tot)[:PINGPONG_FRONT].tolist()]
-    t2 = stencil.time_variants_pingpong(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes, front, halo_z=HALO_Z)
+    t2 = stencil.time_variants_pingpong(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes, front)
     cands2, tot2 = summed(t2)
-    m.variant_times.update({f"{v}@r{r}/pp": round(float(x) / max(1, int(gg.nprocs)), 5)
-                            for (v, r), x in zip(cands2, tot2)})
-    v, r = cands2[int(torch.argmin(tot2))]
+    m.variant_times.update({key(*c) + "/pp": round(float(x) / max(1, int(gg.nprocs)), 5)
+                            for c, x in zip(cands2, tot2)})
+    v, r, hz = cands2[int(torch.argmin(tot2))]
     m.rounds = int(r)
+    m.halo_z = bool(hz)
     return int(v)
 
 

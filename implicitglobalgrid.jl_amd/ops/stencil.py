@@ -82,21 +82,30 @@ SHORTLIST = (0, 2, 9, 11, 14, 21, 23, 24, 25, 26, 40, 43)
 GRID_ROUNDS = (1, 2, 3, 4)
 
 
+def _cand(c, halo_z: bool):
+    """(variant, grid rounds, halo_z) of a candidate: a variant index, a
+    (variant, rounds) pair or a (variant, rounds, halo_z) triple."""
+    if isinstance(c, int):
+        return c, 0, halo_z
+    return (int(c[0]), int(c[1]), bool(c[2]) if len(c) > 2 else halo_z)
+
+
 def time_variants(T2, T, Cp, rd2, dtlam, boxes, candidates=None, reps: int = 5, rounds: int = 3,
                   halo_z: bool = False) -> dict:
     """Median-of-rounds time (ms) of each candidate on these arrays, interleaved
     (the update is pure: T2 = f(T, Cp), so T2 can be scribbled). A candidate is
-    a variant index or a (variant, grid_rounds) pair (grid residency rounds of
-    the launch, see diffusion3d_)."""
+    a variant index, a (variant, grid_rounds) pair (grid residency rounds of
+    the launch, see diffusion3d_) or a (variant, grid_rounds, halo_z) triple
+    (``halo_z`` applies to the others)."""
     n = list(T.shape)
     cands = compiled_variants() if candidates is None else list(candidates)
     s = torch.cuda.current_stream()
     times = {c: [] for c in cands}
 
     def launch(c):
-        v, gr = (c, 0) if isinstance(c, int) else c
+        v, gr, hz = _cand(c, halo_z)
         native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(), boxes, True,
-                           v, s.cuda_stream, gr, halo_z)
+                           v, s.cuda_stream, gr, hz)
 
     for v in cands:  # warm every code object once
         launch(v)
@@ -125,9 +134,9 @@ def time_variants_pingpong(T2, T, Cp, rd2, dtlam, boxes, candidates, steps: int 
     backup = T.clone()
 
     def launch(c, dst, src):
-        v, gr = (c, 0) if isinstance(c, int) else c
+        v, gr, hz = _cand(c, halo_z)
         native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), n, rd2, dtlam, T.element_size(), boxes,
-                           True, v, s.cuda_stream, gr, halo_z)
+                           True, v, s.cuda_stream, gr, hz)
 
     try:
         for c in candidates:
