@@ -93,13 +93,13 @@ def main() -> int:
     mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
     bufs = [T, T2]
 
-    def plain(v, r):
+    def plain(v, r, hz_=False):
         k = [0]
 
         def f():
             src, dst = bufs[k[0] & 1], bufs[(k[0] + 1) & 1]
             native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), [n, n, n], rd2, 1e-4, eb, inner, True,
-                               v, s.cuda_stream, r, hz)
+                               v, s.cuda_stream, r, hz_)
             k[0] += 1
         return f
 
@@ -130,7 +130,9 @@ def main() -> int:
         return {c: sorted(t)[len(t) // 2] for c, t in times.items()}
 
     compiled = set(v for v in range(len(native.diffusion3d_variants())) if native.diffusion3d_variant_compiled(v))
-    pl = bench({f"plain v{v}/r{r}": plain(v, r) for v in PLAIN if v in compiled for r in ROUNDS})
+    forms = (False, True) if hz else (False,)
+    pl = bench({f"plain v{v}/r{r}" + ("/hz" if f else ""): plain(v, r, f)
+                for v in PLAIN if v in compiled for r in ROUNDS for f in forms})
     best_plain = min(pl, key=pl.get)
     print(f"n={n}^3 {a.dtype}: best plain {best_plain} {pl[best_plain]:.4f} ms "
           f"({3 * n ** 3 * eb / pl[best_plain] / 1e6:.0f} GB/s)", flush=True)
@@ -152,7 +154,8 @@ def main() -> int:
         # mode bit 2 compiles the z exchange out: only without a z neighbour
         cands = [c for c in cands if native.diffusion3d_fused_variant_ok(c[0]) and not (has_z and c[1] & 2)]
         fns = {f"v{v}/m{m}/r{r}": fused(fh, v, m, r) for v, m, r in cands}
-        fns["plain"] = plain(*[int(x[1:]) for x in best_plain.split()[1].split("/")])
+        bp = best_plain.split()[1].split("/")
+        fns["plain"] = plain(int(bp[0][1:]), int(bp[1][1:]), len(bp) > 2)
         t = bench(fns)
         if has_z and a.order > 0:
             # z-edge tiles dispatched first (send mode bit 32) at 2..4 residency rounds:
