@@ -154,6 +154,11 @@ __device__ __forceinline__ HxTile<T> hx_tile(const HxScal<T>& a, int64_t bid, in
 // exchange, 0 = the plain update (variants 21+); other subsets served the cost
 // bisect (profiles/r1_fused/feature_bisect_*).
 constexpr int HZ = 262144;
+// Side-only z forms (chosen per wave by diffusion3d_hx_kernel): a z-edge wave
+// holds one z edge unless a row fits in one wave, so the other side's
+// per-row readlanes and selects are compiled out (ZLO: only z = 0 / 1 exchange
+// code, ZHI: only z = n2-1 / n2-2).
+constexpr int ZLO = 524288, ZHI = 1048576;
 
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT>
 __device__ __forceinline__ void
@@ -248,8 +253,9 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   // readfirstlane: the compiler must see zh as uniform, or every readlane
   // with it becomes a waterfall loop draining vmcnt (measured +27 % per step).
   const int zh = __builtin_amdgcn_readfirstlane(static_cast<int>((n2 - VZ - zt) / VZ));
-  const bool zin_lo = (FEAT & 4) && has_lo && zi0, zin_hi = (FEAT & 4) && has_hi && zi1;
-  const bool zout_lo = (FEAT & 8) && has_lo && zo0, zout_hi = (FEAT & 8) && has_hi && zo1;
+  constexpr bool SLO = (FEAT & ZHI) == 0, SHI = (FEAT & ZLO) == 0;  // z sides this form handles
+  const bool zin_lo = SLO && (FEAT & 4) && has_lo && zi0, zin_hi = SHI && (FEAT & 4) && has_hi && zi1;
+  const bool zout_lo = SLO && (FEAT & 8) && has_lo && zo0, zout_hi = SHI && (FEAT & 8) && has_hi && zo1;
   const bool zin = zin_lo || zin_hi, zout = zout_lo || zout_hi;
   // halo_z (FEAT HZ): this wave holds a z edge whose halo element it may write
   const bool hz_wave = (FEAT & HZ) != 0 && ((has_lo && a.zh_lo) || (has_hi && a.zh_hi));
@@ -428,9 +434,14 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         // every row up front made the step wait for all of this plane's loads
         // at once (and per-row branches split the body into blocks the
         // scheduler cannot interleave: profiles/r2_fused_spec/).
-        const T vl = lane_read(zcur, r), vh = lane_read(zcur, 32 + r);
-        tc[r][0] = pl ? vl : tc[r][0];
-        tc[r][VZ - 1] = ph ? vh : tc[r][VZ - 1];
+        if constexpr (SLO) {
+          const T vl = lane_read(zcur, r);
+          tc[r][0] = pl ? vl : tc[r][0];
+        }
+        if constexpr (SHI) {
+          const T vh = lane_read(zcur, 32 + r);
+          tc[r][VZ - 1] = ph ? vh : tc[r][VZ - 1];
+        }
       }
       const V& c = tc[r];
       const V& yv = (r == 0) ? ym : tc[r > 0 ? r - 1 : 0];
@@ -499,9 +510,14 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
           if (zout_hi && lane == zh) zs[3 * RY + r] = out[VZ - 2];
         } else if constexpr ((FEAT & 8) != 0) {
           // branch-free (see the z-in patch): unconditional readlanes + selects
-          const T vl = lane_read(out[1], 0), vh = lane_read(out[VZ - 2], zh);
-          zv = (zout_lo && lane == r) ? vl : zv;
-          zv = (zout_hi && lane == 32 + r) ? vh : zv;
+          if constexpr (SLO) {
+            const T vl = lane_read(out[1], 0);
+            zv = (zout_lo && lane == r) ? vl : zv;
+          }
+          if constexpr (SHI) {
+            const T vh = lane_read(out[VZ - 2], zh);
+            zv = (zout_hi && lane == 32 + r) ? vh : zv;
+          }
         }
       }
     }
@@ -570,6 +586,16 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
 #define IGG_HX_SWEEP(F)                                                                                  \
   hx_sweep<T, BY, RY, VZ, PF, BZ, DF, (F)>(t2, t, cpp, xi0, xi1, yi0, yi1, zi0, zi1, xo0, xo1, yo0, yo1, \
                                            zo0, zo1, a)
+#define IGG_HX_SWEEP_ZS(F)                                                    \
+  do {                                                                        \
+    if constexpr (FZ != 0) {                                                  \
+      if (zs == 1) IGG_HX_SWEEP_R((F) | ZLO);                                 \
+      else if (zs == 2) IGG_HX_SWEEP_R((F) | ZHI);                            \
+      else IGG_HX_SWEEP_R(F);                                                 \
+    } else {                                                                  \
+      IGG_HX_SWEEP_R(F);                                                      \
+    }                                                                         \
+  } while (0)
 #define IGG_HX_SWEEP_R(F)                                                                                \
   hx_sweep<T, BY, RY, VZ, PF, BZ, DF, (F)>(t2, t, cpp, xi0, xi1, yi0, yi1, zi0, zi1, xo0, xo1, yo0, yo1, \
                                            zo0, zo1, a, clo, chi)
@@ -592,9 +618,12 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     // y/z code at all; a 2x2x2 corner rank only the z-edge tiles of one side).
     const bool wx = FX != 0 && ((xs <= 1 && (xi0 || xo0)) || (xe >= n0 - 2 && (xi1 || xo1)));
     const bool wyy = FY != 0 && ((y0 <= 1 && (yi0 || yo0)) || (y0 + nv >= n1 - 1 && (yi1 || yo1)));
-    const bool wzz = FZ != 0 && ((zt == 0 && (zi0 || zo0)) ||
-                                 (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ && (zi1 || zo1)));
+    const bool wz_lo = zt == 0 && (zi0 || zo0);
+    const bool wz_hi = zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ && (zi1 || zo1);
+    const bool wzz = FZ != 0 && (wz_lo || wz_hi);
     int sel = __builtin_amdgcn_readfirstlane((wx ? 1 : 0) | (wyy ? 2 : 0) | (wzz ? 4 : 0));
+    // which z side(s) a z wave holds: 1 low only, 2 high only, 0 both
+    const int zs = __builtin_amdgcn_readfirstlane((wz_lo && !wz_hi) ? 1 : ((wz_hi && !wz_lo) ? 2 : 0));
     if (a.force_sel >= 0) sel = a.force_sel;
     const int64_t t_start = a.stamps ? wall_clock64() : 0;
     // The exchanging waves (sel != 0) synchronise the step with the
@@ -627,10 +656,10 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
         case 1: IGG_HX_SWEEP_R(FK | FX); break;
         case 2: IGG_HX_SWEEP_R(FK | FY); break;
         case 3: IGG_HX_SWEEP_R(FK | FX | FY); break;
-        case 4: IGG_HX_SWEEP_R(FK | FZ); break;
-        case 5: IGG_HX_SWEEP_R(FK | FX | FZ); break;
-        case 6: IGG_HX_SWEEP_R(FK | FY | FZ); break;
-        default: IGG_HX_SWEEP_R(FEAT); break;
+        case 4: IGG_HX_SWEEP_ZS(FK | FZ); break;
+        case 5: IGG_HX_SWEEP_ZS(FK | FX | FZ); break;
+        case 6: IGG_HX_SWEEP_ZS(FK | FY | FZ); break;
+        default: IGG_HX_SWEEP_ZS(FEAT); break;
       }
     }
     if (ks) step_sync_exit(a.sync, threadIdx.x & 63, kc);
@@ -648,6 +677,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
   }
 #undef IGG_HX_SWEEP
 #undef IGG_HX_SWEEP_R
+#undef IGG_HX_SWEEP_ZS
 }
 
 int resident(const void* kernel, int block, size_t lds = 0) {
