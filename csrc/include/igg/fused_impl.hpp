@@ -154,11 +154,14 @@ __device__ __forceinline__ HxTile<T> hx_tile(const HxScal<T>& a, int64_t bid, in
 // exchange, 0 = the plain update (variants 21+); other subsets served the cost
 // bisect (profiles/r1_fused/feature_bisect_*).
 constexpr int HZ = 262144;
-// Side-only z forms (chosen per wave by diffusion3d_hx_kernel): a z-edge wave
-// holds one z edge unless a row fits in one wave, so the other side's
-// per-row readlanes and selects are compiled out (ZLO: only z = 0 / 1 exchange
-// code, ZHI: only z = n2-1 / n2-2).
-constexpr int ZLO = 524288, ZHI = 1048576;
+// Side-only z forms (chosen per wave by diffusion3d_hx_kernel when the tiling
+// has ZSIDES): a z-edge wave holds one z edge unless a row fits in one wave,
+// so the other side's per-row readlanes and selects are compiled out (ZLO:
+// only z = 0 / 1 exchange code, ZHI: only z = n2-1 / n2-2). Opt-in per tiling:
+// the extra sweep instantiations made tilings 11/14 (fused 40/42/44) 4 %
+// slower in every shape, tiling 9 1.2 % faster at a 2x2x2 corner
+// (profiles/r4_shapes/, pass 4).
+constexpr int ZLO = 524288, ZHI = 1048576, ZSIDES = 2097152;
 
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT>
 __device__ __forceinline__ void
@@ -588,7 +591,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
                                            zo0, zo1, a)
 #define IGG_HX_SWEEP_ZS(F)                                                    \
   do {                                                                        \
-    if constexpr (FZ != 0) {                                                  \
+    if constexpr (FZ != 0 && (FEAT & ZSIDES) != 0) {                          \
       if (zs == 1) IGG_HX_SWEEP_R((F) | ZLO);                                 \
       else if (zs == 2) IGG_HX_SWEEP_R((F) | ZHI);                            \
       else IGG_HX_SWEEP_R(F);                                                 \

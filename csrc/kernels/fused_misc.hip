@@ -11,7 +11,7 @@ bool dispatch_misc(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode
 #ifdef IGG_PROBES  // measured, not adopted
     case 2: launch_mode<T, 4, 4, 2, true, 1>(d, io, mode, s); break;
 #endif
-    case 9: launch_mode<T, 4, 8, 4, false, 1>(d, io, mode, s); break;
+    case 9: launch_mode<T, 4, 8, 4, false, 1, ZSIDES>(d, io, mode, s); break;  // + side-only z forms
     case 14: launch_mode<T, 2, 8, 4, false, 2>(d, io, mode, s); break;
     // + edge-lane z exchange (FEAT 8192: no per-row v_readlane, which the
     // one-wave-per-SIMD f32 form of tiling 14 cannot hide: profiles/r2_f32_fused/)
