@@ -73,6 +73,24 @@ FUSED_DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
 FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4), (44, 36, 4))
 # (send mode bit 32 = z-edge tiles dispatched first: the f32 2x2x2 corner's best
 # form at 4 grid rounds; slower for f64 at every round count, profiles/r4_shapes/)
+# Win record of the fused forms (rounds 2-4: the bench's A/Bs on every box and
+# rehearsal, profiles/r4_shapes/ per rank shape; the in-kernel-sync forms, bit
+# 16, are derived from the front later): tried first, so a spent A/B budget
+# (IGG_BENCH_AB_BUDGET) drops forms that never won anywhere.
+#   (9, 8, 3)  8-rank 2x2x2 rehearsal winner (r4), (9, 0, 3) 2x2x2 corner (r4 pass 4)
+#   (42, 12, 2) interior + corner f64 (m28 = 12|16), (42, 9, 2) x+/xy+ (m25 = 9|16)
+#   (14, 8, 3) f32 x/xy (m24 = 8|16), (44, 44, 4) / (44, 12, 4) f32 corner
+FUSED_WIN_ORDER = ((9, 8, 3), (42, 12, 2), (42, 9, 2), (9, 0, 3), (42, 8, 2), (14, 8, 3), (44, 44, 4),
+                   (44, 12, 4), (42, 4, 2), (0, 12, 3), (42, 0, 2), (40, 12, 2))
+
+
+def _win_order(cands: list) -> list:
+    """``cands`` with the forms of FUSED_WIN_ORDER first (in that order, if
+    present), then the rest in their listed order."""
+    first = [c for c in FUSED_WIN_ORDER if c in cands]
+    return first + [c for c in cands if c not in first]
+
+
 BASELINE_PER_GPU_GBS = 23.0  # BASELINE.md, derived T_eff per P100 GPU
 METRIC = ("effective GB/s per GPU + weak-scaling parallel efficiency, "
           "3-D diffusion 512^3/GPU at 1/2/4/8 MI355X")
@@ -251,12 +269,152 @@ def _bracket(comm) -> None:
 
 
 def _timed(model, comm, k: int) -> float:
-    _sync(comm)
+    return _timed_fn(model.run, comm, k)[0]
+
+
+def _timed_fn(run, comm, k: int) -> tuple[float, float]:
+    """Seconds per step of ``run(k)`` between two barrier+synchronize
+    brackets: (MAX over ranks, this rank's own)."""
+    if _BRACKET["gpu"]:
+        _sync(comm)
     _bracket(comm)
     t0 = time.perf_counter()
-    model.run(k)
+    run(k)
     _bracket(comm)
-    return _max_over_ranks(comm, time.perf_counter() - t0) / k
+    own = time.perf_counter() - t0
+    return _max_over_ranks(comm, own) / k, own / k
+
+
+def _all_ranks(comm, v: float) -> list:
+    """``v`` of every rank, in rank order (gloo all-gather)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.float64)
+    if comm.size == 1:
+        return [float(v)]
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(comm.size)]
+    dist.all_gather(out, t, group=comm.gloo)
+    return [float(x.item()) for x in out]
+
+
+# Same-process weak-scaling efficiency (config.efficiency): interleaved pairs
+# of [the local problem, the multi-rank step], medians.
+EFF_PAIRS = 3
+LOCAL_GRAPH_STEPS = 10
+
+
+def _median(xs):
+    s = sorted(xs)
+    return s[len(s) // 2] if len(s) % 2 else 0.5 * (s[len(s) // 2 - 1] + s[len(s) // 2])
+
+
+def measure_efficiency(model, comm, log, graph: bool, k: int, pairs: int = EFF_PAIRS) -> dict | None:
+    """Weak-scaling efficiency measured in THIS job: E = t_it(local) / t_it(step).
+
+    ``t_it(step)``: the model's step as the timed region runs it (exchange
+    included: update_halo_ or the fused exchange; hipGraph replays).
+    ``t_it(local)``: the identical local problem as the 1-GPU run times it -
+    the same plain stencil (variant, grid rounds, z-edge form) on the same
+    arrays, no exchange (update_halo_ with PROC_NULL neighbours is a no-op,
+    src/update_halo.jl:40-42), replayed from its own hipGraph - on every rank
+    at once, so both numbers come from the same GPUs, processes, clocks and
+    brackets (MAX over ranks each). ``pairs`` interleaved [local, step] pairs
+    of ``k`` steps, medians. This removes the box-to-box spread (+-2-3 %)
+    that a ratio of two different jobs' numbers carries (E(N) =
+    t_it(1) / t_it(N)). Collective. The halo planes are left unexchanged by
+    the local steps: the caller takes any starting-state snapshot afterwards
+    (the model is told with ``mark_modified``)."""
+    if not hasattr(model, "local_step"):
+        return None
+    k = max(2, k + (k % 2))  # even: the ping-pong buffers keep their roles
+    on_gpu = getattr(model, "device", None) is not None and model.device.type == "cuda"
+    gl = None
+    if on_gpu and graph:
+        from igg.parallel.halo import capture_graph
+
+        def rec():
+            for _ in range(LOCAL_GRAPH_STEPS):
+                model.local_step()
+
+        model.local_step()
+        model.local_step()
+        try:
+            gl = capture_graph(rec, "bench.local_problem", uses_halo=False)
+        except Exception as e:
+            log(f"efficiency: local-problem capture failed, eager ({type(e).__name__}: {e})"[:200])
+            gl = None
+        # every rank replays or none (the timings must be of the same form)
+        if _max_over_ranks(comm, 0.0 if gl is not None else 1.0) > 0:
+            gl = None
+
+    def run_local(n):
+        if gl is not None:
+            for _ in range(n // LOCAL_GRAPH_STEPS):
+                gl.replay()
+            n %= LOCAL_GRAPH_STEPS
+        for _ in range(n):
+            model.local_step()
+
+    tl, tm, own_l, own_m = [], [], [], []
+    for _ in range(pairs):
+        a, b = _timed_fn(run_local, comm, k)
+        tl.append(a)
+        own_l.append(b)
+        a, b = _timed_fn(model.run, comm, k)
+        tm.append(a)
+        own_m.append(b)
+    used_graph, gl = gl is not None, None
+    if hasattr(model, "mark_modified"):
+        model.mark_modified()  # the local steps wrote the fields outside the exchange protocol
+    t_loc, t_step = _median(tl), _median(tm)
+    per_rank_loc = _all_ranks(comm, _median(own_l))
+    per_rank_step = _all_ranks(comm, _median(own_m))
+    eff = t_loc / t_step if t_step > 0 else None
+    log(f"efficiency (same process, {pairs} interleaved pairs x {k} steps, medians): local "
+        f"{t_loc * 1e3:.4f} ms, step {t_step * 1e3:.4f} ms -> E = {eff:.4f}")
+    return {
+        "value": round(eff, 5) if eff is not None else None,
+        "definition": "t_it(local problem) / t_it(step), same job: every rank times the identical local "
+                      "problem of the 1-GPU run (plain stencil, no exchange) interleaved with the real step; "
+                      "medians of the MAX over ranks",
+        "t_local_ms": round(t_loc * 1e3, 5),
+        "t_step_ms": round(t_step * 1e3, 5),
+        "pairs": pairs,
+        "steps": k,
+        "local_ms_samples": [round(x * 1e3, 5) for x in tl],
+        "step_ms_samples": [round(x * 1e3, 5) for x in tm],
+        "per_rank_local_ms": [round(x * 1e3, 5) for x in per_rank_loc],
+        "per_rank_step_ms": [round(x * 1e3, 5) for x in per_rank_step],
+        "per_rank_efficiency": [round(a / t_step, 5) if t_step > 0 else None for a in per_rank_loc],
+        "local_graph": used_graph,
+    }
+
+
+class _ABBudget:
+    """Total wall budget of the A/B stages (IGG_BENCH_AB_BUDGET seconds,
+    default 150): candidates are tried in the order of their win record and
+    the rest is skipped once the budget is spent. ``left()`` is collective
+    (every rank takes the same decision: the MAX of the ranks' elapsed time)."""
+
+    def __init__(self, comm, seconds: float | None = None):
+        self.comm = comm
+        self.seconds = float(os.environ.get("IGG_BENCH_AB_BUDGET", "150")) if seconds is None else seconds
+        self.t0 = time.monotonic()
+        self.skipped: list = []
+
+    def elapsed(self) -> float:
+        return time.monotonic() - self.t0
+
+    def left(self) -> bool:
+        return _max_over_ranks(self.comm, self.elapsed()) <= self.seconds
+
+
+AB_BUDGET = None  # _ABBudget of the run (set in main)
+# Host-side record of the stages around the timed region, in execution order
+# (config.stage_order; tests/test_bench.py checks that nothing - no snapshot
+# allocation or copy, no check - runs between the warm load and the bracket).
+ORDER: list = []
 
 
 def _timed_candidate(model, comm, k: int, graph: bool) -> float:
@@ -272,15 +430,16 @@ def _timed_candidate(model, comm, k: int, graph: bool) -> float:
     return _timed(model, comm, k)
 
 
-def _step_estimate_ms(model, comm) -> float:
-    """ms per step of the current schedule: one untimed replay (or step),
-    MAX over ranks so every rank runs the same number of warm-up steps."""
+def _step_estimate_ms(model, comm) -> tuple[float, int]:
+    """(ms per step of the current schedule, steps run): one untimed replay
+    (or step), MAX over ranks so every rank runs the same number of warm-up
+    steps."""
     k = model.graph_steps if getattr(model, "graph", None) is not None else 1
     _sync(comm)
     t0 = time.perf_counter()
     model.run(k)
     _sync(comm)
-    return max(0.05, _max_over_ranks(comm, (time.perf_counter() - t0) * 1e3 / k))
+    return max(0.05, _max_over_ranks(comm, (time.perf_counter() - t0) * 1e3 / k)), k
 
 
 class _NoPhases:
@@ -558,7 +717,10 @@ def select_transport(model, comm, log, valid: dict, graph: bool) -> tuple[str, d
     if not cands:
         raise RuntimeError("no device transport passed the bitwise validation against the host-staged path")
     times = {}
-    for name, t, mode, ov in cands:
+    for i, (name, t, mode, ov) in enumerate(cands):
+        if i > 0 and AB_BUDGET is not None and not AB_BUDGET.left():
+            AB_BUDGET.skipped.append(name)
+            continue
         PH.enter(f"ab:{name}", "overlap" if ov else _transport_key(t), deadline=300)
         H.set_transport(t)
         H.set_halo_mode(mode)
@@ -721,6 +883,7 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
         # every form also with its exchanged x planes peeled off the chunk sweep
         # (send mode bit 8: profiles/r2_peel/, -1.8 % f64 / -2.8 % f32 interior rank)
         cands += [(v, fm | 8, gr) for v, fm, gr in cands]
+        cands = _win_order(cands)
         if os.environ.get("IGG_FUSED_CANDIDATES"):  # "v/mode/rounds,..." (measurements)
             cands = [tuple(int(x) for x in c.split("/")) for c in os.environ["IGG_FUSED_CANDIDATES"].split(",")]
     else:
@@ -737,14 +900,24 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
 
     def timing_passes(cs):
         nonlocal t_unf
-        for _ in range(2):
+        for p in range(2):
+            if p > 0 and AB_BUDGET is not None and not AB_BUDGET.left():
+                break  # the first pass's numbers stand
             PH.enter("fused:ab:update_halo", unf_key, deadline=300)
             model.set_fused(False)
             t_unf = min(t_unf, _timed_candidate(model, comm, 20, graph))
             model.set_fused(True)
-            for c in cs:
+            for i, c in enumerate(cs):
                 if times.get(c) == float("inf"):
                     continue  # failed in the first pass
+                if p > 0 and c not in times:
+                    continue  # skipped for the budget in the first pass
+                # the first candidate of the first pass always runs (the
+                # record's best form); later ones while the budget lasts
+                if (p > 0 or i > 0) and AB_BUDGET is not None and not AB_BUDGET.left():
+                    if p == 0:
+                        AB_BUDGET.skipped.extend(name(x) for x in cs[i:])
+                    break
                 use(c)
                 PH.enter(f"fused:ab:{name(c)}", ckey(c), deadline=300)
                 err = ""
@@ -775,9 +948,14 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
     # excluded by the supervisor after a failure). Its kept check below is the
     # same 200-step bitwise check; if it fails, the next fastest form - a
     # sync-kernel one - is kept.
-    if (diffusion and "fused-inkernel" not in EXCL and model._fh is not None
-            and model._fh.in_kernel_sync_for(16) and not model._fh.in_kernel_sync_for(0)
-            and os.environ.get("IGG_FUSED_INKERNEL", "1") != "0"):
+    # The gate depends on per-rank facts (a rank shares its GPU, the
+    # IGG_FUSED_SYNC_KERNEL of its environment): every rank takes it only if
+    # every rank can (timing_passes is collective; a split decision would leave
+    # some ranks waiting in its collectives until the phase deadline).
+    inkernel_ok = (diffusion and "fused-inkernel" not in EXCL and model._fh is not None
+                   and model._fh.in_kernel_sync_for(16) and not model._fh.in_kernel_sync_for(0)
+                   and os.environ.get("IGG_FUSED_INKERNEL", "1") != "0")
+    if diffusion and _max_over_ranks(comm, 0.0 if inkernel_ok else 1.0) == 0.0:
         front = [c for c, _t in sorted(times.items(), key=lambda kv: kv[1]) if not c[1] & 16][:2]
         timing_passes([(v, fm | 16, gr) for v, fm, gr in front])
     model.set_fused(False)
@@ -838,6 +1016,7 @@ def _save_start(model, pre: dict) -> None:
     on one GPU did not fit two)."""
     import torch
 
+    ORDER.append("snapshot")
     cmp = _compared(model)
     for nm in _state(model):
         src = getattr(model, nm)
@@ -866,9 +1045,10 @@ def _restore_start(model, pre: dict) -> None:
         model.mark_modified()
 
 
-def stencil_post_check(model, comm, log, pre: dict, k: int, on_gpu: bool) -> dict:
+def stencil_post_check(model, comm, log, pre: dict, k: int, on_gpu: bool, timed_steps: int | None = None) -> dict:
     """After the timed region (update_halo_ path, any N): restore the state
-    the timed steps started from, run the same ``k`` steps eagerly with a
+    of the snapshot taken before the warm load, run the same ``k`` steps
+    (warm load + timed steps: ``timed_steps`` of them timed) eagerly with a
     SECOND compiled stencil variant (bitwise interchangeable by construction,
     tests/test_gpu_stencil.py) and compare the result bitwise with the field
     the timed steps produced. A mismatch means the timed run computed a wrong
@@ -890,7 +1070,7 @@ def stencil_post_check(model, comm, log, pre: dict, k: int, on_gpu: bool) -> dic
     if not _all_ok(comm, why):
         res = why or "failed on another rank"
         log(f"post-timing stencil check: could not start ({res})")
-        return {"steps": k, "variant": v_timed, "check_variant": v2, "result": res}
+        return {"steps": k, "timed_steps": timed_steps, "variant": v_timed, "check_variant": v2, "result": res}
     try:
         _restore_start(model, pre)
         model.graph = None
@@ -920,8 +1100,9 @@ def stencil_post_check(model, comm, log, pre: dict, k: int, on_gpu: bool) -> dic
         model.graph = graph
     fails = _max_over_ranks(comm, 1.0 if why else 0.0)
     res = "ok" if fails == 0.0 else (why or "failed on another rank")
-    log(f"post-timing stencil check ({k} steps, variant {v_timed} vs {v2 if v2 is not None else 'same'}): {res}")
-    return {"steps": k, "variant": v_timed, "check_variant": v2, "result": res}
+    log(f"post-timing stencil check ({k} steps from the pre-warm-load snapshot, variant {v_timed} vs "
+        f"{v2 if v2 is not None else 'same'}): {res}")
+    return {"steps": k, "timed_steps": timed_steps, "variant": v_timed, "check_variant": v2, "result": res}
 
 
 def validate_host_matching(field, comm, log) -> dict:
@@ -967,7 +1148,11 @@ def validate_host_matching(field, comm, log) -> dict:
     return res
 
 
+T_START = time.monotonic()
+
+
 def main():
+    global AB_BUDGET
     args = parse()
     import faulthandler
 
@@ -1040,12 +1225,15 @@ def main():
     graph_ok = args.graph and on_gpu and "graph" not in EXCL
     _BRACKET["gpu"], _BRACKET["dev"] = on_gpu, False
     valid, ab = None, None
+    AB_BUDGET = _ABBudget(comm)  # the transport + fused A/B stages share one wall budget
+    AB_BUDGET.elapsed_at_end = 0.0
     if on_gpu and nprocs > 1:
         ref = "staged"
         names = None if args.transport == "auto" else [c[0] for c in TRANSPORT_CANDIDATES if c[1] == args.transport]
         if args.share_gpu:  # ranks share one device: RCCL refuses duplicate GPUs
             names = ["put"]
         valid = validate_transports(field(), comm, log, ref=ref, names=names)
+        AB_BUDGET.t0 = time.monotonic()  # the budget covers the A/B timing, not the correctness checks
         _BRACKET["dev"] = bool(comm.rccl is not None and valid.get("rccl-sequential") == "ok")
         if args.share_gpu and valid.get("put") != "ok":
             H.set_transport("staged")
@@ -1063,6 +1251,9 @@ def main():
     fused_ab = None
     if on_gpu and not args.overlap and (nprocs > 1 or args.loopback or pdims):
         fused_ab = select_fused(model, comm, log, args.fused, graph_ok)
+    AB_BUDGET.elapsed_at_end = AB_BUDGET.elapsed() if (valid is not None or fused_ab is not None) else 0.0
+    if AB_BUDGET.skipped:
+        log(f"A/B budget ({AB_BUDGET.seconds:.0f} s) spent: skipped {', '.join(AB_BUDGET.skipped)}")
     PH.enter("warmup", _path_key(model), deadline=300)
     for _ in range(args.warmup):
         model.step()
@@ -1075,35 +1266,60 @@ def main():
             graph_error = f"{type(e).__name__}: {e}"[:200]
             model.graph = None
             log(f"hipGraph capture failed, running eager: {graph_error}")
-    # Steady-state warm-up through the timed path: MI355X needs ~10-20 ms of
-    # continuous load after a lighter phase (autotune launches with host syncs,
-    # capture) before its clocks settle; the first two 10-step replays after
-    # capture measured 5-7 % slower (profiles/r2_gap/NOTES.md). So the W
-    # requested warm-up steps are followed by enough untimed graph replays to
-    # keep the GPU busy for IGG_BENCH_WARM_MS (default 40 ms) right before the
-    # timed region. The timed region itself is unchanged: exactly K full steps.
-    extra = 0
-    warm_ms = float(os.environ.get("IGG_BENCH_WARM_MS", "40"))
-    PH.enter("warmup", _path_key(model), deadline=300)
-    if on_gpu and warm_ms > 0:
-        est = _step_estimate_ms(model, comm)
-        k = max(1, getattr(model, "graph_steps", 1) if getattr(model, "graph", None) is not None else 1)
-        extra = int(-(-warm_ms // (est * k))) * k
-        model.run(extra)
+    # Same-process weak-scaling efficiency (config.efficiency): interleaved
+    # pairs of the 1-GPU run's local problem and the real step, on these GPUs
+    # and processes. Before the snapshot and the warm load below: it leaves the
+    # halo planes unexchanged, which no later check depends on.
+    eff = None
+    if os.environ.get("IGG_BENCH_EFFICIENCY", "1") != "0":
+        PH.enter("efficiency", _path_key(model), deadline=300)
+        eff = measure_efficiency(model, comm, log, graph_ok, args.steps)
+        ORDER.append("efficiency")
     pre = {}  # the state a non-fused timed region starts from (stencil_post_check)
+    warm = {"extra": None, "since_snapshot": 0}
+
+    def warm_load():
+        """Snapshot, then the untimed warm load, then NOTHING but the timed
+        region's bracket. The post-timing stencil check replays every step
+        from the snapshot (warm load + timed steps), so its buffers are
+        allocated and copied here, before the warm load, never between the
+        warm load and the bracket (round 4 lost 2.9 % of the driver's
+        20-step number to a 1 GiB snapshot taken right before the bracket).
+        Steady-state warm-up through the timed path: MI355X needs ~10-20 ms
+        of continuous load after a lighter phase (autotune launches with host
+        syncs, capture, this snapshot) before its clocks settle; the first
+        two 10-step replays after capture measured 5-7 % slower
+        (profiles/r2_gap/NOTES.md). So the W requested warm-up steps are
+        followed by enough untimed replays to keep the GPU busy for
+        IGG_BENCH_WARM_MS (default 40 ms) right before the timed region,
+        which is unchanged: exactly K full steps."""
+        PH.enter("warmup", _path_key(model), deadline=300)
+        if not getattr(model, "fused", False):
+            _save_start(model, pre)
+        else:
+            pre.clear()
+        since = 0
+        warm_ms = float(os.environ.get("IGG_BENCH_WARM_MS", "40"))
+        if on_gpu and warm_ms > 0:
+            if warm["extra"] is None:
+                est, k_est = _step_estimate_ms(model, comm)
+                since += k_est
+                k = max(1, getattr(model, "graph_steps", 1) if getattr(model, "graph", None) is not None else 1)
+                warm["extra"] = int(-(-warm_ms // (est * k))) * k
+            model.run(warm["extra"])
+            since += warm["extra"]
+        warm["since_snapshot"] = since
+        ORDER.append("warm_load")
+
     timed_graph = [False]  # whether the last timed region replayed a hipGraph
 
     def timed_region() -> float:
         """The timed region: exactly ``args.steps`` full steps (plus the
         configured gathers) between two barrier+synchronize brackets; MAX over
-        ranks of the wall time. The starting state is saved first (outside the
-        brackets) for the post-timing stencil check."""
+        ranks of the wall time. Preceded directly by ``warm_load``."""
         PH.enter("timed", _path_key(model), deadline=600)
-        if not getattr(model, "fused", False):
-            _save_start(model, pre)
-        else:
-            pre.clear()
         timed_graph[0] = getattr(model, "graph", None) is not None
+        ORDER.append("timed")
         sync()
         _bracket(comm)
         t0 = time.perf_counter()
@@ -1134,6 +1350,7 @@ def main():
         t1 = time.perf_counter()
         return _max_over_ranks(comm, t1 - t0)
 
+    warm_load()
     elapsed = timed_region()
     H.check_transport()
     if hasattr(model, "check"):
@@ -1161,7 +1378,7 @@ def main():
             model.graph = None
             if graph_ok:
                 model.capture()
-            model.run(extra)  # the same untimed warm load as before the first region
+            warm_load()  # snapshot + the same untimed warm load as before the first region
             elapsed = timed_region()
             H.check_transport()
     post_valid = None
@@ -1185,7 +1402,7 @@ def main():
             model.graph = None
             if graph_ok:
                 model.capture()
-            model.run(extra)
+            warm_load()
             elapsed = timed_region()
             H.check_transport()
             failed = post_valid
@@ -1197,7 +1414,9 @@ def main():
     stencil_post = None
     if pre and not getattr(model, "fused", False):
         PH.enter("post:stencil", _path_key(model), deadline=300)
-        stencil_post = stencil_post_check(model, comm, log, pre, args.steps, on_gpu)
+        ORDER.append("stencil_post_check")
+        stencil_post = stencil_post_check(model, comm, log, pre, warm["since_snapshot"] + args.steps, on_gpu,
+                                          timed_steps=args.steps)
         if stencil_post["result"] != "ok":
             log(f"bench: post-timing stencil check failed ({stencil_post['result']}): no result")
             raise SystemExit(1)
@@ -1291,7 +1510,13 @@ def main():
                 "stencil_variant": getattr(model, "variant", None),
                 "stencil_variant_ms": getattr(model, "variant_times", None),
                 "finite": finite,
-                "warmup_steps_run": args.warmup + extra,
+                "warmup_steps_run": args.warmup + (warm["extra"] or 0),
+                "efficiency": eff,
+                "stage_order": list(ORDER),
+                "ab_wall_s": round(AB_BUDGET.elapsed_at_end, 2) if AB_BUDGET is not None else None,
+                "ab_budget_s": AB_BUDGET.seconds if AB_BUDGET is not None else None,
+                "ab_skipped_for_budget": (AB_BUDGET.skipped or None) if AB_BUDGET is not None else None,
+                "wall_s": round(time.monotonic() - T_START, 2),
                 "loopback_emulation": bool(args.loopback),
                 "self_launched": os.environ.get("IGG_BENCH_SELF_LAUNCHED") == "1",
                 "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),

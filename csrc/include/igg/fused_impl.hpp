@@ -37,12 +37,21 @@ namespace igg {
 extern int64_t* g_hx_stamps;
 extern int g_hx_force_sel;
 
-// Fused launches by tiling family, one translation unit each (compiled in
-// parallel): fused_t0.hip (variants 0, 50), fused_t11.hip (11, 40, 41),
-// fused_misc.hip (2, 9, 14). Return false for a variant not in the family.
-bool fused_launch_t0(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
-bool fused_launch_t11(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
-bool fused_launch_misc(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
+// Fused launches by tiling family and element type, one translation unit each
+// so they compile in parallel (the tiling-9 family with its side-only z forms
+// alone took 7.7 min as one unit of both types): fused_t0_<dt>.hip (variants
+// 0, 50), fused_t11_<dt>.hip (40, 42), fused_t9_<dt>.hip (9),
+// fused_t14_<dt>.hip (14, 44); the bodies are in igg/fused_families.hpp, each
+// unit instantiates one (family, type). Return false for a variant not in the
+// family.
+template <typename T>
+bool fused_family_t0(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
+template <typename T>
+bool fused_family_t11(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
+template <typename T>
+bool fused_family_t9(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
+template <typename T>
+bool fused_family_t14(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s);
 
 namespace {
 

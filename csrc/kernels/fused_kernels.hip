@@ -1,7 +1,7 @@
 // Fused halo-exchange diffusion kernel for gfx950 (see igg/fused.hpp): the
 // restrict-argument plain sweeps (stencil variants 21+) and the entry points.
 // The kernel templates live in igg/fused_impl.hpp; the fused instantiations in
-// fused_t0.hip / fused_t11.hip / fused_misc.hip (one tiling family each).
+// fused_t{0,11,9,14}_{f64,f32}.hip (one tiling family and type each).
 #include "igg/fused_impl.hpp"
 
 namespace igg {
@@ -18,19 +18,22 @@ namespace {
 template <typename T>
 void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
   const HaloIOArgs none{};
-  switch (v) {  // tilings of the shortlisted restrict-form variants 21/23/24/25/26/40/43
+  switch (v) {  // tilings of the shortlisted restrict-form variants 21/24/26/40/43
     // each tiling in the partial-line and the whole-line (HZ, halo_z) z-edge
     // store form: the autotune times both (models/diffusion3d.py)
 #define IGG_PLAIN_HX(BY, RY, VZ, BZ, F)                                         \
   (d.halo_z ? launch_hx<T, BY, RY, VZ, false, BZ, false, (F) | HZ>(d, none, s) \
             : launch_hx<T, BY, RY, VZ, false, BZ, false, (F)>(d, none, s))
     case 0: IGG_PLAIN_HX(4, 4, 4, 1, 0); break;
-    case 9: IGG_PLAIN_HX(4, 8, 4, 1, 0); break;
     case 11: IGG_PLAIN_HX(4, 8, 2, 1, 0); break;
-    case 14: IGG_PLAIN_HX(2, 8, 4, 2, 0); break;
     case 100: IGG_PLAIN_HX(2, 8, 2, 1, 0); break;
     case 124: IGG_PLAIN_HX(4, 8, 2, 1, 512 | 1024); break;
     case 141: IGG_PLAIN_HX(2, 8, 2, 4, 0); break;
+#ifdef IGG_PROBES
+    // restrict forms of tilings 9 and 14 (variants 23, 25): no A/B win in rounds 2-4
+    case 9: IGG_PLAIN_HX(4, 8, 4, 1, 0); break;
+    case 14: IGG_PLAIN_HX(2, 8, 4, 2, 0); break;
+#endif
 #undef IGG_PLAIN_HX
 #ifdef IGG_PROBES
     // measured and not adopted (rounds 1-2): other tilings, non-temporal Cp,
@@ -99,9 +102,15 @@ void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int 
   if (mode < 0 || mode > 63 || (mode & 16))
     fail("diffusion3d (fused halo): send mode must be 0..63 without bit 16 (step sync: FusedHalo)");
   if (a.elem_bytes != 8 && a.elem_bytes != 4) fail("diffusion3d: only float32/float64 are supported");
-  if (!fused_launch_t0(a, io, variant, mode, stream) && !fused_launch_t11(a, io, variant, mode, stream) &&
-      !fused_launch_misc(a, io, variant, mode, stream))
-    fail("diffusion3d (fused halo): variant ", variant, " has no fused instantiation");
+  const bool ok = a.elem_bytes == 8 ? (fused_family_t0<double>(a, io, variant, mode, stream) ||
+                                       fused_family_t11<double>(a, io, variant, mode, stream) ||
+                                       fused_family_t9<double>(a, io, variant, mode, stream) ||
+                                       fused_family_t14<double>(a, io, variant, mode, stream))
+                                    : (fused_family_t0<float>(a, io, variant, mode, stream) ||
+                                       fused_family_t11<float>(a, io, variant, mode, stream) ||
+                                       fused_family_t9<float>(a, io, variant, mode, stream) ||
+                                       fused_family_t14<float>(a, io, variant, mode, stream));
+  if (!ok) fail("diffusion3d (fused halo): variant ", variant, " has no fused instantiation");
 }
 
 }  // namespace igg

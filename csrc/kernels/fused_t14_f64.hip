@@ -1,0 +1,7 @@
+// Fused halo-exchange diffusion kernels, tiling 14: fused variants 14, 44 (double).
+// One (family, element type) per translation unit: igg/fused_families.hpp.
+#include "igg/fused_families.hpp"
+
+namespace igg {
+template bool fused_family_t14<double>(const DiffusionArgs&, const HaloIOArgs&, int, int, hipStream_t);
+}  // namespace igg

@@ -504,17 +504,19 @@ KArgs<T> make_args(const DiffusionArgs& a) {
 }  // namespace
 
 // Compiled variants of the default build: the autotune shortlist
-// (ops/stencil.py SHORTLIST), the fallbacks its restrict-form variants use for
-// other boxes, the scalar fallback (1) and the one-row slab kernel (18). The
-// other tilings were measured in rounds 1-2 and lost; they are built only with
-// `build.py --probes` (IGG_PROBES) for re-measurement.
+// (ops/stencil.py SHORTLIST: the variants that won an A/B on some box in rounds
+// 2-4), the plain tilings the fused/overlap paths and the restrict-form
+// variants fall back to for other boxes (0, 5, 9, 11, 14), the scalar fallback
+// (1) and the one-row slab kernel (18). The other tilings were measured in
+// rounds 1-4 and never won; they are built only with `build.py --probes`
+// (IGG_PROBES) for re-measurement.
 bool stencil_variant_compiled(int v) {
 #ifdef IGG_PROBES
   return v >= 0 && v < NVARIANTS;
 #else
   switch (v) {
     case 0: case 1: case 2: case 5: case 9: case 11: case 14: case 18:
-    case 21: case 23: case 24: case 25: case 26: case 40: case 43:
+    case 21: case 24: case 26: case 40: case 43:
       return true;
     default:
       return false;

@@ -36,8 +36,17 @@ PeerMesh::PeerMesh(int rank, int nranks, AllGather allgather)
     (void)gethostname(host, sizeof(host) - 1);
     const std::string id = std::string(host) + "/" + bus;
     const std::vector<std::string> ids = allgather_(id);
-    for (int r = 0; r < static_cast<int>(ids.size()); ++r)
-      if (r != rank_ && ids[r] == id) shares_device_ = true;
+    // Collective by construction: every rank sees the same id list, so if ANY
+    // two ranks share a device, every rank treats the mesh as shared (the
+    // step-sync form must be the same on all ranks, igg/fused.hpp; a rank-local
+    // answer split the bench's in-kernel-sync A/B gate when ranks shared GPUs
+    // unevenly, e.g. 3 ranks on 2 GPUs).
+    for (int r = 0; r < static_cast<int>(ids.size()) && !shares_device_; ++r)
+      for (int q = r + 1; q < static_cast<int>(ids.size()); ++q)
+        if (ids[r] == ids[q]) {
+          shares_device_ = true;
+          break;
+        }
   }
   if (const char* m = std::getenv("IGG_PUT_ARENA_MIN")) {
     const long long mb = std::atoll(m);

@@ -195,6 +195,16 @@ class Acoustic2D:
         self.Vy, self.Vy2 = self.Vy2, self.Vy
         self._warm = True
 
+    def local_step(self) -> None:
+        """One step of the LOCAL problem (what a rank without neighbours runs:
+        the staggered update, no exchange - update_halo_ with PROC_NULL
+        neighbours is a no-op, reference src/update_halo.jl:40-42). Timing
+        only (the bench's same-process efficiency); halos stay unexchanged."""
+        self._update(self.P2, self.Vx2, self.Vy2, self.P, self.Vx, self.Vy)
+        self.P, self.P2 = self.P2, self.P
+        self.Vx, self.Vx2 = self.Vx2, self.Vx
+        self.Vy, self.Vy2 = self.Vy2, self.Vy
+
     def capture(self, steps: int = GRAPH_STEPS) -> None:
         """hipGraph of ``steps`` (even) time steps: buffers are back in their
         roles after a replay; replay launch overhead (~9 us on MI355X) is paid

@@ -418,6 +418,19 @@ class Diffusion3D:
         self.T, self.T2 = T2, T
         self._warm = True
 
+    def local_step(self) -> None:
+        """One step of the LOCAL problem: what a rank without neighbours runs
+        (the N = 1 run of the weak-scaling curve): the plain stencil with this
+        model's variant, grid rounds and z-edge store form on the whole
+        interior; update_halo_ with PROC_NULL neighbours is a no-op
+        (reference: src/update_halo.jl:40-42, no neighbour -> nothing sent).
+        Used by the bench's same-process efficiency E = t(local) / t(step).
+        Leaves the halo planes unexchanged: timing only (callers that go on
+        with real steps call ``mark_modified`` afterwards)."""
+        T, T2 = self.T, self.T2
+        stencil.diffusion3d_(T2, T, self.Cp, boxes=self.inner, halo_z=self.halo_z, **self._kw())
+        self.T, self.T2 = T2, T
+
     def capture(self, steps: int = None) -> None:
         """Record ``steps`` (even, default GRAPH_STEPS) time steps in a hipGraph for ``run``.
 
@@ -598,7 +611,9 @@ def _choose_variant(m: "Diffusion3D") -> int:
     # biased low and the alternating buffers cost ~1 % (profiles/r2_gap/), so
     # the pick is made on what the run actually does.
     front = [cands[i] for i in torch.argsort(tot)[:PINGPONG_FRONT].tolist()]
-    t2 = stencil.time_variants_pingpong(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes, front)
+    # 5 interleaved rounds of 20 steps, medians: the front differs by less
+    # than the box noise of one sample (the round-4 picks varied run to run)
+    t2 = stencil.time_variants_pingpong(m.T2, m.T, m.Cp, rd2, m.dt * m.lam, boxes, front, steps=20, rounds=5)
     cands2, tot2 = summed(t2)
     m.variant_times.update({key(*c) + "/pp": round(float(x) / max(1, int(gg.nprocs)), 5)
                             for c, x in zip(cands2, tot2)})

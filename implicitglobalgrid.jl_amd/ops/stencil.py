@@ -70,12 +70,13 @@ def _variant_for(T, boxes, rd2, dtlam, T2, Cp, stream) -> int:
     return v
 
 
-# Variants that win somewhere on MI355X (sweeps in profiles/): v4_by4_ry4_nt,
-# v2_by4_ry4_pf_nt, v4_by4_ry4, v4_by4_ry8_nt, v2_by4_ry8_nt, v4_bz2_by2_ry8_nt.
-# 21+: restrict-argument (fused-kernel) form; 40: lane-distributed z-segment edge
-# loads at one workgroup per CU (profiles/r1_zl/); 43: full-row z tiles
-# (profiles/r2_fullrow/).
-SHORTLIST = (0, 2, 9, 11, 14, 21, 23, 24, 25, 26, 40, 43)
+# The variants that won the autotune on some box in rounds 2-4 (the bench's
+# 512^3 f64 / 1024^3 f32 configs, profiles/ and BENCH_r0*.json): 40, 24, 43,
+# 11, 2 (f64), 14, 21, 26 (f32 and both). 21+: restrict-argument (fused-kernel)
+# form; 40: lane-distributed z-segment edge loads at one workgroup per CU
+# (profiles/r1_zl/); 43: full-row z tiles (profiles/r2_fullrow/). 0, 9, 23 and
+# 25 never won a real config in rounds 2-4 (23/25 are --probes builds now).
+SHORTLIST = (2, 11, 14, 21, 24, 26, 40, 43)
 # Grid residency rounds tried per variant by the model autotune: 1-4 measured
 # best depending on the box and variant (profiles/r1_fused/grid.log,
 # variant_sweep.log, r1_zl/: 1-2.5 %).

@@ -425,8 +425,8 @@ def _run_torchrun(argv, max_attempts, timeout, poll, env_adjust):
                 st = []
                 for r in range(size):
                     x = g.get(f"a{attempt}/s{r}")
-                    if x is None:  # not reported yet: running since the attempt began
-                        x = {"exit": None, "phase": "start", "since": now, "deadline": DEFAULT_DEADLINE}
+                    if x is None:  # not reported yet: running since the attempt began (as in _run_local)
+                        x = {"exit": None, "phase": "start", "since": t_start, "deadline": DEFAULT_DEADLINE}
                     st.append(x)
                 verdict = decide(st, now, excl, max_attempts - attempt)
                 if verdict is None and time.monotonic() > t_end:

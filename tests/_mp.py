@@ -26,6 +26,29 @@ def free_port() -> int:
 MAX_TIMEOUT = 170.0
 
 
+class TierBudget:
+    """Wall budget of a tier of multi-rank launches (tests/test_multigpu.py):
+    each launch gets ``min(MAX_TIMEOUT, what is left)`` and none starts with
+    less than ``min_launch`` seconds left (it is skipped instead), so the
+    tier's worst case - every launch hitting its bound - is ``seconds`` plus
+    the teardown of the last launch, whatever the number of launches. The
+    clock starts at the first launch (collection and the single-GPU tests
+    before the tier do not count)."""
+
+    def __init__(self, seconds: float, min_launch: float = 30.0, clock=time.monotonic):
+        self.seconds, self.min_launch, self.clock = float(seconds), float(min_launch), clock
+        self.t0 = None
+
+    def next_timeout(self) -> float | None:
+        """The bound of the next launch, or None when the budget is spent."""
+        if self.t0 is None:
+            self.t0 = self.clock()
+        left = self.seconds - (self.clock() - self.t0)
+        if left < self.min_launch:
+            return None
+        return min(MAX_TIMEOUT, left)
+
+
 def run_ranks(nprocs: int, scenario: str, *args, timeout: float = 150.0, env_extra=None) -> list[str]:
     """Run ``scenario`` on ``nprocs`` ranks. Fail-fast: the first rank that
     exits non-zero stops the others (a dead rank would otherwise leave its

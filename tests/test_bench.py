@@ -158,3 +158,55 @@ def test_share_gpu_post_timing_checks(inject):
         assert c["fused_halo"] is False
     else:
         assert fp["result"] == "ok" and c["fused_halo"] is True
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_efficiency_measured_in_the_same_job(n):
+    """config.efficiency: interleaved pairs of the 1-GPU run's local problem
+    (plain stencil, no exchange) and the real step, on the same processes;
+    value = median t_local / median t_step, with per-rank numbers."""
+    r, rec = _run(["--gpus", str(n), "--device", "cpu", "--n", "20", "--steps", "4", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    e = rec["config"]["efficiency"]
+    assert e is not None and e["pairs"] >= 3 and e["steps"] % 2 == 0
+    assert len(e["local_ms_samples"]) == e["pairs"] == len(e["step_ms_samples"])
+    assert abs(e["value"] - e["t_local_ms"] / e["t_step_ms"]) <= 1e-3 * e["value"] + 1e-4
+    assert len(e["per_rank_local_ms"]) == n == len(e["per_rank_efficiency"])
+
+
+def test_nothing_between_warm_load_and_bracket():
+    """The post-check snapshot (allocation + copy) is taken BEFORE the warm
+    load, and the timed region's bracket follows the warm load directly (round
+    4 lost 2.9 % of the driver's 20-step number to a snapshot in between); the
+    stencil post check replays the warm load + the timed steps."""
+    r, rec = _run(["--gpus", "1", "--device", "cpu", "--n", "20", "--steps", "4", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    order = rec["config"]["stage_order"]
+    i = order.index("timed")
+    assert order[i - 1] == "warm_load", order
+    assert order[i - 2] == "snapshot", order
+    assert "efficiency" in order[:i - 2], order
+    sp = rec["config"]["stencil_post_check"]
+    assert sp["result"] == "ok" and sp["timed_steps"] == 4 and sp["steps"] >= 4
+
+
+def test_ab_budget_orders_and_truncates():
+    """The A/B budget is collective and the fused candidates are tried in the
+    order of their win record (a spent budget drops the never-winners)."""
+    import importlib.util as ilu
+
+    spec = ilu.spec_from_file_location("bench_mod", BENCH)
+    b = ilu.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    cands = [(0, 0, 3), (42, 12, 2), (9, 8, 3), (50, 1, 2)]
+    assert b._win_order(cands) == [(9, 8, 3), (42, 12, 2), (0, 0, 3), (50, 1, 2)]
+
+    class _C:
+        size = 1
+
+    bud = b._ABBudget(_C(), seconds=0.0)
+    import time as _t
+
+    _t.sleep(0.01)
+    assert not bud.left()
+    assert b._ABBudget(_C(), seconds=100.0).left()

@@ -9,21 +9,24 @@ node with ``python -m pytest tests -m multigpu``.
 
 First-run-proof budget: the checks are chained into suites, one launch of the
 ranks per suite (tests/mp_worker.py scenario_suite: one torch import and one
-rendezvous per launch, the grid re-initialised per item), and every launch is
-bounded by tests/_mp.py MAX_TIMEOUT = 170 s (fail-fast: the first failing rank
-stops the others and names the item). The tier is 10 launches:
+rendezvous per launch, the grid re-initialised per item). The WHOLE tier has
+one wall budget (tests/_mp.py TierBudget, IGG_MGPU_TIER_BUDGET, default
+480 s): each launch is bounded by min(170 s, what is left) and a launch that
+would start with < 30 s left is skipped, so the tier's worst case is the
+budget, not launches x 170 s; with the single-GPU tests (<= 300 s) that
+stays inside the driver's 900 s step cap. The launches run in the order of
+their value, so a spent budget drops the least essential ones:
 
-    1  8-rank direct-z fused soak (first: the least proven path the bench may pick)
-    2  8-rank fused exchange forms + diffusion vs the global-grid run
-    3  8-rank halo oracle (RCCL sequential / one-phase / auto, put) + ring
+    1  8-rank halo oracle (RCCL sequential / one-phase / auto, put) + ring
+    2  2-rank suite (left == right periodic neighbour: same-peer ordering)
+    3  4-rank suite (2x2x1)
     4  8-rank gather (pull and RCCL paths, roots 0 and 7) + gather_async + collectives
-    5  2-rank suite (left == right periodic neighbour: same-peer ordering; fused)
-    6  4-rank suite (2x2x1)
-    7, 8  bench.py --gpus 2 / --gpus 8 self-launch (validation + post-timing checks)
+    5  8-rank fused exchange forms + diffusion vs the global-grid run
+    6, 7  bench.py --gpus 2 / --gpus 8 self-launch (validation + post-timing checks)
+    8  8-rank direct-z fused soak
     9, 10 2- and 4-rank direct-z fused soak
 
-Worst case (every launch hitting its bound): 10 x 170 s = 28.3 min; expected
-on a healthy node: about 3-4 min (each suite item takes seconds).
+Expected on a healthy node: about 3-4 min (each suite item takes seconds).
 
 Reference counterparts: test/test_update_halo.jl (halo oracle incl. dims=2
 periodic, where left == right neighbour), :697-743 (ring), test/test_gather.jl
@@ -36,7 +39,7 @@ import sys
 
 import pytest
 
-from tests._mp import MAX_TIMEOUT, ROOT, run_ranks
+from tests._mp import ROOT, TierBudget, run_ranks
 
 pytestmark = [pytest.mark.gpu, pytest.mark.multigpu]
 
@@ -76,33 +79,24 @@ def halo(cfg, env):
     return f"halo:mgpu:{':'.join(map(str, cfg))}:f64|{env}"
 
 
+TIER = TierBudget(float(os.environ.get("IGG_MGPU_TIER_BUDGET", "480")))
+
+
+def _launch_timeout() -> float:
+    t = TIER.next_timeout()
+    if t is None:
+        pytest.skip(f"multigpu tier budget ({TIER.seconds:.0f} s) spent")
+    return t
+
+
 def suite(nprocs, *items):
     need(nprocs)
-    outs = run_ranks(nprocs, "suite", *items, timeout=MAX_TIMEOUT)
+    outs = run_ranks(nprocs, "suite", *items, timeout=_launch_timeout())
     for o in outs:
         assert f"suite OK ({len(items)} items" in o, o[-3000:]
 
 
-# 1. the direct-z fused soak first (direct z: the z faces land in the halo
-#    column of the neighbour's next field; random host skew between rounds)
-def test_direct_z_fused_soak_8_ranks():
-    suite(8, soak(40, 4), soak(42, 12), soak(0, 1))
-
-
-# 2. fused exchange forms and the 8-rank diffusion vs one global array
-def test_fused_forms_and_diffusion_8_ranks():
-    suite(8,
-          fused(0, 1, 18, 20, 40, 7, 0, 0),
-          fused(0, 0, 16, 18, 24, 6, 1, 1),
-          fused(42, 4, 18, 20, 136, 5, 0, 1),
-          fused(0, 5, 16, 18, 24, 6, 1, 1),
-          fused(40, 8, 34, 66, 136, 5, 1, 1),
-          fused(44, 4, 18, 20, 136, 4, 1, 0),
-          f"diffusion:mgpu:24:20:18:7:0|{RCCL}",
-          f"diffusion:mgpu:24:20:18:7:0|{PUT}")
-
-
-# 3. halo oracle (every boundary plane, edges and corners, bitwise)
+# 1. halo oracle (every boundary plane, edges and corners, bitwise)
 def test_halo_and_ring_8_ranks():
     items = []
     for cfg in ((7, 5, 6, 0, 0, 0), (7, 5, 6, 1, 1, 1)):
@@ -113,16 +107,7 @@ def test_halo_and_ring_8_ranks():
     suite(8, *items)
 
 
-# 4. gather (pull path and RCCL path, roots 0 and N-1), gather_async, collectives
-def test_gather_and_collectives_8_ranks():
-    suite(8,
-          f"gather:mgpu:f64|{RCCL}",
-          f"gather:mgpu:f64|{RCCL};IGG_GATHER_PULL=0",
-          f"gather_async|{PUT}",
-          f"collectives:mgpu|{RCCL}")
-
-
-# 5. two ranks: periodic dims=2 makes left == right (same-peer ordering)
+# 2. two ranks: periodic dims=2 makes left == right (same-peer ordering)
 def test_suite_2_ranks():
     suite(2,
           *[halo((7, 5, 6, 1, 1, 1), f"{RCCL};IGG_HALO_MODE={m}") for m in ("sequential", "onephase", "auto")],
@@ -137,7 +122,7 @@ def test_suite_2_ranks():
           fused(42, 12, 40, 66, 136, 6, 1, 0))
 
 
-# 6. four ranks (2x2x1)
+# 3. four ranks (2x2x1)
 def test_suite_4_ranks():
     suite(4,
           *[halo((9, 6, 5, 1, 0, 1), f"{RCCL};IGG_HALO_MODE={m}") for m in ("sequential", "onephase", "auto")],
@@ -148,7 +133,29 @@ def test_suite_4_ranks():
           f"diffusion:mgpu:24:20:18:5:0|{RCCL}")
 
 
-# 7, 8. the bench on N distinct GPUs
+# 4. gather (pull path and RCCL path, roots 0 and N-1), gather_async, collectives
+def test_gather_and_collectives_8_ranks():
+    suite(8,
+          f"gather:mgpu:f64|{RCCL}",
+          f"gather:mgpu:f64|{RCCL};IGG_GATHER_PULL=0",
+          f"gather_async|{PUT}",
+          f"collectives:mgpu|{RCCL}")
+
+
+# 5. fused exchange forms and the 8-rank diffusion vs one global array
+def test_fused_forms_and_diffusion_8_ranks():
+    suite(8,
+          fused(0, 1, 18, 20, 40, 7, 0, 0),
+          fused(0, 0, 16, 18, 24, 6, 1, 1),
+          fused(42, 4, 18, 20, 136, 5, 0, 1),
+          fused(0, 5, 16, 18, 24, 6, 1, 1),
+          fused(40, 8, 34, 66, 136, 5, 1, 1),
+          fused(44, 4, 18, 20, 136, 4, 1, 0),
+          f"diffusion:mgpu:24:20:18:7:0|{RCCL}",
+          f"diffusion:mgpu:24:20:18:7:0|{PUT}")
+
+
+# 6, 7. the bench on N distinct GPUs
 @pytest.mark.parametrize("nprocs", [2, 8])
 def test_bench_self_launch_validates_every_transport(nprocs):
     """bench.py --gpus N (self-launched, one rank per GPU) validates RCCL
@@ -156,10 +163,12 @@ def test_bench_self_launch_validates_every_transport(nprocs):
     timing, checks the timed schedule (and the fused exchange, if kept) after
     timing, and reports n_gpus == N."""
     need(nprocs)
+    t = _launch_timeout()
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["IGG_BENCH_AB_BUDGET"] = "40"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nprocs), "--n", "128",
-                        "--steps", "20", "--warmup", "2", "--launch-timeout", "150"],
-                       capture_output=True, text=True, timeout=MAX_TIMEOUT, env=env, cwd=ROOT)
+                        "--steps", "20", "--warmup", "2", "--launch-timeout", str(max(20, int(t) - 20))],
+                       capture_output=True, text=True, timeout=t, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     c = rec["config"]
@@ -169,6 +178,12 @@ def test_bench_self_launch_validates_every_transport(nprocs):
     if c["fused_halo"]:
         assert c["fused_post_check"]["result"] == "ok", c["fused_post_check"]
     assert c["finite"]
+
+
+# 8. the direct-z fused soak (direct z: the z faces land in the halo
+#    column of the neighbour's next field; random host skew between rounds)
+def test_direct_z_fused_soak_8_ranks():
+    suite(8, soak(40, 4), soak(42, 12), soak(0, 1))
 
 
 # 9, 10. direct-z soak at 2 and 4 ranks
