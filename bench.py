@@ -71,6 +71,14 @@ FUSED_DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
 # f32 (1024^3 config): tiling 14 with the edge-lane z exchange (fused variant
 # 44) is the fastest fused form there (profiles/r2_f32_fused/).
 FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4), (44, 36, 4))
+# z unpack (send mode bit 64, FusedHalo::Z_UNPACK): the z sends go into the
+# neighbours' arenas as coalesced whole-line stores, the sweep has no z receive
+# code, and a copy kernel writes the received z faces into the next T's halo
+# column after the step synchronisation - the z exchange out of the sweep's
+# receive path without direct z's scattered 8-B remote stores. With a z
+# neighbour only (without one these equal their mode & ~64 forms).
+FUSED_ZUNPACK = ((9, 64, 3), (42, 64, 2), (40, 64, 2), (0, 64, 3))
+FUSED_ZUNPACK_F32 = ((44, 64, 4), (14, 64, 3))
 # (send mode bit 32 = z-edge tiles dispatched first: the f32 2x2x2 corner's best
 # form at 4 grid rounds; slower for f64 at every round count, profiles/r4_shapes/)
 # Win record of the fused forms (rounds 2-4: the bench's A/Bs on every box and
@@ -80,8 +88,11 @@ FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4), (44, 36, 4))
 #   (9, 8, 3)  8-rank 2x2x2 rehearsal winner (r4), (9, 0, 3) 2x2x2 corner (r4 pass 4)
 #   (42, 12, 2) interior + corner f64 (m28 = 12|16), (42, 9, 2) x+/xy+ (m25 = 9|16)
 #   (14, 8, 3) f32 x/xy (m24 = 8|16), (44, 44, 4) / (44, 12, 4) f32 corner
-FUSED_WIN_ORDER = ((9, 8, 3), (42, 12, 2), (42, 9, 2), (9, 0, 3), (42, 8, 2), (14, 8, 3), (44, 44, 4),
-                   (44, 12, 4), (42, 4, 2), (0, 12, 3), (42, 0, 2), (40, 12, 2))
+#   (9, 72, 3) / (42, 72, 2): the round-5 z-unpack corner forms (no record yet;
+#   right behind the record's front so a spent budget still times them)
+FUSED_WIN_ORDER = ((9, 8, 3), (42, 12, 2), (42, 9, 2), (9, 0, 3), (9, 72, 3), (42, 72, 2), (42, 8, 2),
+                   (14, 8, 3), (44, 44, 4), (44, 12, 4), (44, 72, 4), (42, 4, 2), (0, 12, 3), (42, 0, 2),
+                   (40, 12, 2))
 
 
 def _win_order(cands: list) -> list:
@@ -880,6 +891,10 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
             cands += FUSED_DIRECT
             if model.T.dtype.itemsize == 4:
                 cands += FUSED_DIRECT_F32
+        if any(model.sides[2]):
+            cands += FUSED_ZUNPACK
+            if model.T.dtype.itemsize == 4:
+                cands += FUSED_ZUNPACK_F32
         # every form also with its exchanged x planes peeled off the chunk sweep
         # (send mode bit 8: profiles/r2_peel/, -1.8 % f64 / -2.8 % f32 interior rank)
         cands += [(v, fm | 8, gr) for v, fm, gr in cands]
@@ -956,7 +971,8 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
                    and model._fh.in_kernel_sync_for(16) and not model._fh.in_kernel_sync_for(0)
                    and os.environ.get("IGG_FUSED_INKERNEL", "1") != "0")
     if diffusion and _max_over_ranks(comm, 0.0 if inkernel_ok else 1.0) == 0.0:
-        front = [c for c, _t in sorted(times.items(), key=lambda kv: kv[1]) if not c[1] & 16][:2]
+        # (the z-unpack forms, bit 64, always use the sync kernel: no in-kernel twin)
+        front = [c for c, _t in sorted(times.items(), key=lambda kv: kv[1]) if not c[1] & (16 | 64)][:2]
         timing_passes([(v, fm | 16, gr) for v, fm, gr in front])
     model.set_fused(False)
     model.graph = None

@@ -34,13 +34,17 @@ import torch  # noqa: E402
 import igg  # noqa: E402
 from igg._native import native  # noqa: E402
 
-PLAIN = (0, 2, 9, 11, 14, 24, 25, 40, 43)
+PLAIN = (2, 11, 14, 21, 24, 26, 40, 43)  # ops/stencil.py SHORTLIST
 ROUNDS = (1, 2, 3)
 # bench.py FUSED_CANDIDATES / FUSED_DIRECT / FUSED_DIRECT_F32 (+ peel bit 8)
 FUSED = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (9, 0, 3), (14, 0, 3), (40, 0, 2), (42, 0, 2), (42, 1, 2), (50, 0, 2),
          (11, 0, 2), (11, 2, 2), (11, 8, 2), (11, 10, 2), (14, 0, 2), (9, 0, 2))
 DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
 DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4))
+# z unpack (send mode bit 64, FusedHalo::Z_UNPACK): arena z sends, no z receive
+# in the sweep, a copy kernel writes the received z faces after the step sync
+ZUNPACK = ((9, 64, 3), (42, 64, 2), (40, 64, 2), (0, 64, 3))
+ZUNPACK_F32 = ((44, 64, 4), (14, 64, 3))
 
 
 def neighbours(shape: str):
@@ -148,6 +152,7 @@ def main() -> int:
         cands = list(base)
         if not a.candidates and any(nb[2][s_] >= 0 for s_ in range(2)):
             cands += list(DIRECT) + (list(DIRECT_F32) if eb == 4 else [])
+            cands += list(ZUNPACK) + (list(ZUNPACK_F32) if eb == 4 else [])
         if not a.candidates:
             cands += [(v, m | 8, r) for v, m, r in cands]
         has_z = any(nb[2][s_] >= 0 for s_ in range(2))
@@ -174,7 +179,9 @@ def main() -> int:
             for k, v_ in to.items():
                 t[k] = min(t.get(k, float("inf")), v_)
         if a.inkernel > 0:  # the fastest forms again with the step sync inside the kernel
-            front = sorted((c for c in t if c != "plain"), key=t.get)[:a.inkernel]
+            # (z unpack, bit 64, always uses the sync kernel: no in-kernel form)
+            front = sorted((c for c in t if c != "plain" and not int(c.split("/")[1][1:]) & 64),
+                           key=t.get)[:a.inkernel]
             fk = {}
             for c in front:
                 v, m, r = (int(x[1:]) for x in c.split("/"))

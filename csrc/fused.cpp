@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <vector>
 
+#include "igg/copy.hpp"
+
 namespace igg {
 
 FusedHalo::FusedHalo(std::shared_ptr<PeerMesh> mesh, const std::array<int64_t, 3>& n, int elem_bytes,
@@ -63,7 +65,7 @@ void FusedHalo::set_fields(uintptr_t a, uintptr_t b) {
   fields_ = mesh_->map_buffers({a, b});  // collective
 }
 
-HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z) const {
+HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z, bool z_unpack) const {
   HaloIOArgs io{};
   const int64_t eb = elem_;
   const int64_t wh = (step & 1) * half_, rh = ((step + 1) & 1) * half_;
@@ -77,6 +79,13 @@ HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z)
       if (primed) io.in[d][s] = reinterpret_cast<uintptr_t>(mine + (rh + off_[d][s]) * eb);
     }
   io.zpitch = zp_;
+  // Whole-line z-edge stores (HaloIOArgs::zh), explicit per side: allowed
+  // where nobody else writes t2's z halo column during the kernel.
+  for (int s = 0; s < 2; ++s) io.zh[s] = 1;
+  io.z_out_arena = true;
+  if (direct_z && z_unpack) fail("FusedHalo: direct z and z unpack are exclusive send modes");
+  if (z_unpack)
+    for (int s = 0; s < 2; ++s) io.in[2][s] = 0;  // the z halo comes from the field (unpack_z of the last step)
   if (direct_z && (nb_[2][0] != PROC_NULL || nb_[2][1] != PROC_NULL)) {
     if (fields_.empty()) fail("FusedHalo: direct z needs the field buffers (set_fields)");
     const char* mine_t2 = reinterpret_cast<const char*>(t2);
@@ -93,11 +102,38 @@ HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z)
       // + n2 absorbs the kernel's (y-1) row index.
       const int64_t col = (s == 0 ? n2 - 1 : 0) + n2;
       io.out[2][s] = reinterpret_cast<uintptr_t>(fields_.at(r).at(k) + col * eb);
+      io.zh[s] = 0;  // this side's halo column receives the neighbour's direct-z stores during the kernel
     }
     io.zpitch = n1 * n2;
     io.zrow = n2;
+    io.z_out_arena = false;
   }
   return io;
+}
+
+void FusedHalo::unpack_z(int64_t step, uintptr_t t2, hipStream_t stream) const {
+  // My arena half (step & 1) holds, at region off_[2][s], the z plane the
+  // neighbour at side s computed in its step `step` (layout x*zp + (y-1),
+  // x in [1, n0-2], y in [1, n1-2]): my z halo at side s (z = 0 / n2-1) of
+  // t2 for those rows - the only rows of the halo column a sweep reads.
+  const int64_t n0 = n_[0], n1 = n_[1], n2 = n_[2], eb = elem_;
+  const char* mine = mesh_->arena(mesh_->rank()) + (step & 1) * half_ * eb;
+  std::vector<Copy2D> cs;
+  for (int s = 0; s < 2; ++s) {
+    if (nb_[2][s] == PROC_NULL) continue;
+    const int64_t col = s == 0 ? 0 : n2 - 1;
+    Copy2D c;
+    c.src = mine + (off_[2][s] + 1 * zp_) * eb;
+    c.dst = reinterpret_cast<char*>(t2) + ((1 * n1 + 1) * n2 + col) * eb;
+    c.n_outer = n0 - 2;
+    c.n_inner = n1 - 2;
+    c.src_so = zp_;
+    c.src_si = 1;
+    c.dst_so = n1 * n2;
+    c.dst_si = n2;
+    cs.push_back(c);
+  }
+  launch_copy2d(cs, static_cast<int>(eb), stream);
 }
 
 void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed,
@@ -106,7 +142,9 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
     if (a.n[d] != n_[d]) fail("FusedHalo.step: field shape does not match the fused halo's local grid");
   if (a.elem_bytes != elem_) fail("FusedHalo.step: field dtype does not match the fused halo");
   if (entry) sync(stream);  // entry barrier (fused.hpp)
-  HaloIOArgs x = io(step, primed, a.t2, (mode & 4) != 0);
+  const bool zu = (mode & Z_UNPACK) != 0 && (nb_[2][0] != PROC_NULL || nb_[2][1] != PROC_NULL);
+  if (zu && (mode & 4)) fail("FusedHalo.step: send mode bits 4 (direct z) and 64 (z unpack) are exclusive");
+  HaloIOArgs x = io(step, primed, a.t2, (mode & 4) != 0, zu);
   // Step synchronisation: the 1-wave sync kernel after the stencil (default:
   // rehearsed with 8 ranks, and as fast as the in-kernel form,
   // profiles/r3_boxes/), or inside the kernel (put.hpp StepSync) with send
@@ -115,12 +153,18 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
   // rank's kernel needs: the forced 8-rank shared-GPU rehearsal timed out).
   // IGG_FUSED_SYNC_KERNEL / set_step_sync override both.
   bool used = false;
-  if (in_kernel_sync(mode) && sync_.n_out > 0) {  // no neighbour: nothing to synchronise in the kernel
+  // (z unpack: the unpack must follow the step's synchronisation, so the
+  // sync-kernel form always)
+  if (!zu && in_kernel_sync(mode) && sync_.n_out > 0) {  // no neighbour: nothing to synchronise in the kernel
     x.sync = step_sync_from(sync_);
     x.sync_used = &used;
   }
-  launch_diffusion3d_fused(a, x, variant, mode & ~IN_KERNEL_SYNC, stream);
+  // the kernel form: z unpack = the no-z-receive form (bit 4's kernel) with
+  // the z sends into the arena (x.out[2], zrow 1)
+  const int kmode = (mode & ~(IN_KERNEL_SYNC | Z_UNPACK)) | (zu ? 4 : 0);
+  launch_diffusion3d_fused(a, x, variant, kmode, stream);
   if (!used) sync(stream);
+  if (zu) unpack_z(step, a.t2, stream);
   open_ = used;
 }
 

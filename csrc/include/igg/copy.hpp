@@ -33,7 +33,8 @@ struct CopyBatch {
   Copy2D c[MAX_BATCH];
   int64_t block_start[MAX_BATCH + 1];
   int n;
-  uint32_t flat_mask = 0;  // bit c: copy c has short rows -> one element per lane
+  uint32_t flat_mask = 0;    // bit c: copy c has short rows -> one element per lane
+  uint32_t gather_mask = 0;  // bit c: long rows with a strided side (z faces of a C-ordered field)
   // Put transport: a device-resident exchange epoch selects the arena half;
   // parity_side 1 shifts every dst, 2 every src by parity_bytes when odd.
   const uint64_t* epoch = nullptr;

@@ -31,6 +31,9 @@
 // that for fine-grained memory only, so across devices the fields must be
 // fine-grained (Diffusion3D's default field_memory="fine"). docs/COHERENCE.md
 // has the whole argument.
+// Z unpack (mode bit 64): z sends into the arena as in the default form, but
+// the z halo is read from the field by the next sweep, written there by a copy
+// kernel after the step's synchronisation (unpack_z) - see Z_UNPACK below.
 // Results are bitwise identical to stencil + update_halo_ (tests/test_fused.py).
 #pragma once
 
@@ -60,7 +63,11 @@ class FusedHalo {
   // `direct_z`, the z sends target the halo column of the neighbour's buffer
   // that corresponds to `t2` (set_fields) and nothing is read from the arena
   // along z.
-  HaloIOArgs io(int64_t step, bool primed, uintptr_t t2 = 0, bool direct_z = false) const;
+  // With `z_unpack` (send mode bit Z_UNPACK), the z sends go into the
+  // neighbours' arenas (whole-line coalesced stores) and nothing is read from
+  // the arena along z in the kernel: unpack_z() writes the received z faces
+  // into t2's halo column after the step synchronisation.
+  HaloIOArgs io(int64_t step, bool primed, uintptr_t t2 = 0, bool direct_z = false, bool z_unpack = false) const;
   // Collective: the two ping-pong field buffers of this rank (same order on
   // every rank, registered at the same step); needed by direct z (mode bit 4).
   // Every rank swaps them in lockstep, so "my t2 is buffer k" means "each
@@ -94,6 +101,17 @@ class FusedHalo {
   void set_step_sync(int mode) { sync_mode_ = mode; }
   // Send mode bit selecting the in-kernel step synchronisation (step()).
   static constexpr int IN_KERNEL_SYNC = 16;
+  // Send mode bit of the z-unpack form (a 2x2x2 corner rank's z exchange out
+  // of the sweep's receive path): the z-edge waves keep only their coalesced
+  // arena send (one whole-line store per x step; no per-row patch of a
+  // received halo, no scattered 8-B remote stores as with direct z), and after
+  // the sync kernel a copy kernel writes the received z faces (my arena, this
+  // step's half) into t2's z halo column, which the next sweep reads like any
+  // other element. Needs the sync-kernel form (bit 16 is ignored with it) and
+  // excludes direct z (bit 4).
+  static constexpr int Z_UNPACK = 64;
+  // The unpack of the z-unpack form (after the step synchronisation of `step`).
+  void unpack_z(int64_t step, uintptr_t t2, hipStream_t stream) const;
   // Whether a step with send mode `mode` synchronises inside the kernel.
   bool in_kernel_sync(int mode = 0) const;
 

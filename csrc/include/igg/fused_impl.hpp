@@ -734,6 +734,12 @@ int64_t hx_feature_waves(int64_t n0, int64_t n1, int64_t n2, int64_t ch, int64_t
   return nch * nty * BY * ntz * BZ - qx * qy * qz;
 }
 
+// Whole-line z-edge stores allowed at z side s (HaloIOArgs::zh; -1: no
+// neighbour or an arena z input there).
+inline bool zh_side(const HaloIOArgs& io, int s) {
+  return io.zh[s] >= 0 ? io.zh[s] != 0 : (io.in[2][s] != 0 || io.out[2][s] == 0);
+}
+
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
 void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream, bool peel = false,
                bool order = false) {
@@ -775,8 +781,8 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   // value: T2's halo planes are stale by design in fused mode and rewritten by
   // sync_halo; nobody else writes them). Not with direct z: the neighbour
   // stores into exactly that element while this kernel runs.
-  a.zh_lo = (d.halo_z && (io.in[2][0] || !io.out[2][0])) ? 1 : 0;
-  a.zh_hi = (d.halo_z && (io.in[2][1] || !io.out[2][1])) ? 1 : 0;
+  a.zh_lo = (d.halo_z && zh_side(io, 0)) ? 1 : 0;
+  a.zh_hi = (d.halo_z && zh_side(io, 1)) ? 1 : 0;
   a.sync = StepSync{};
   // In-kernel step sync: the specialised kernel only (per-wave feature
   // classes), and not under the diagnostics that override the classes.
@@ -842,6 +848,11 @@ void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStre
     // receivers' field halo elements, so the z-edge waves read their halo
     // from the field like every other wave and carry only the send code.
     if (io.in[2][0] || io.in[2][1]) fail("diffusion3d (fused halo): direct z mode with z arena input");
+    // halo_z contract (HaloIOArgs::zh): a side whose halo column a neighbour
+    // writes during this kernel (direct z) never takes whole-line edge stores
+    for (int sd = 0; sd < 2; ++sd)
+      if (d.halo_z && io.out[2][sd] && !io.z_out_arena && zh_side(io, sd))
+        fail("diffusion3d (fused halo): whole-line z-edge stores on a direct-z side (HaloIOArgs::zh)");
     if (mode & 1) launch_hx<T, BY, RY, VZ, PF, BZ, true, 203 | XF | HZ>(d, io, s, pk, ord);
     else launch_hx<T, BY, RY, VZ, PF, BZ, false, 203 | XF | HZ>(d, io, s, pk, ord);
   } else if (zx || !(mode & 2)) {

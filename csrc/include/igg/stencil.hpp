@@ -73,6 +73,17 @@ struct HaloIOArgs {
   uintptr_t out[3][2];
   int64_t zpitch;
   int64_t zrow;
+  // Whole-line z-edge stores (DiffusionArgs::halo_z) per z side: 1 allowed
+  // (no other writer of t2's halo column at that side during the kernel: no
+  // neighbour, the arena z exchange, or the z-unpack form whose unpack kernel
+  // rewrites the column after the step), 0 forbidden (direct z: the
+  // neighbour stores into exactly that element while this kernel runs), -1
+  // derived from in/out (no neighbour or an arena z input: allowed). FusedHalo
+  // sets them explicitly; launch_mode rejects an allowed side that receives
+  // direct-z stores (z_out_arena false).
+  int zh[2] = {-1, -1};
+  // The z sends (out[2]) go into arena regions, not into a neighbour's field.
+  bool z_out_arena = true;
   // In-kernel step synchronisation (put.hpp StepSync; FusedHalo): the launch
   // takes it when it can count its exchanging waves and then sets *sync_used
   // (otherwise the caller follows the kernel with the sync kernel).
@@ -89,8 +100,8 @@ void fused_debug(int64_t* stamps, int force_sel);
 // (tiling = a fused-capable variant index); used by the "hx" variants.
 void launch_diffusion3d_inner_hx(const DiffusionArgs& a, int tiling, hipStream_t stream);
 // mode 0: sends stored as computed; 1: deferred one x step; + 2: z-edge exchange
-// compiled out when there is no z neighbour; + 4: direct z (see HaloIOArgs and
-// fused_impl.hpp launch_mode).
+// compiled out when there is no z neighbour; + 4: no z receive code (direct z,
+// or FusedHalo's z-unpack form; see HaloIOArgs and fused_impl.hpp launch_mode).
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,
                               hipStream_t stream);
 void host_diffusion3d(const DiffusionArgs& a, const std::vector<Box>& boxes);

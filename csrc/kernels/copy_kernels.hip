@@ -9,15 +9,24 @@
 // Rows with unit stride on both sides move 4 elements per lane in flight.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "igg/copy.hpp"
 #include "igg/sysstore.hpp"
 
 namespace igg {
+
+extern bool g_copy_gather;
+
 namespace {
 
 constexpr int BLOCK = 256;
 constexpr int EPT = 4;                         // elements per thread per chunk
 constexpr int64_t CHUNK = BLOCK * EPT;         // elements of a row per workgroup
+// Strided rows (gather path): a wave covers 64 consecutive inner elements of
+// GROWS outer rows, so each lane keeps GROWS independent line loads in flight;
+// a workgroup is 4 such waves (4 * GROWS outer rows).
+constexpr int GROWS = 8;
 
 struct alignas(16) B16 { uint64_t x, y; };
 
@@ -57,6 +66,33 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
       const int64_t o = e / cp.n_inner, i = e - o * cp.n_inner;
       store<T, FENCE>(reinterpret_cast<T*>(dbase) + o * cp.dst_so + i * cp.dst_si,
                       reinterpret_cast<const T*>(sbase)[o * cp.src_so + i * cp.src_si]);
+    }
+  } else if ((batch.gather_mask >> c) & 1u) {
+    // A face of a C-ordered field across its fastest dim (z): every element
+    // of the row sits in its own cache line on the strided side, so the copy
+    // is bound by how many line requests are in flight, not by bytes. The
+    // row-chunk path put one 512-element row in a 1024-element workgroup
+    // (half the lanes idle, 2 loads per lane, one workgroup per row: 2 x 514
+    // workgroups for a 512^3 z face pair - 19.7 us, profiles/r4_trace/); here
+    // the block decode is scalar and every lane issues GROWS loads before its
+    // first store.
+    const int64_t nic = (cp.n_inner + 63) / 64;
+    const int64_t og = local / nic, ic = local - og * nic;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t i = ic * 64 + lane;
+    const int64_t o0 = (og * 4 + w) * GROWS;
+    if (i < cp.n_inner && o0 < cp.n_outer) {
+      const T* __restrict__ src = reinterpret_cast<const T*>(sbase) + i * cp.src_si;
+      T* __restrict__ dst = reinterpret_cast<T*>(dbase) + i * cp.dst_si;
+      const int nr = static_cast<int>(min<int64_t>(GROWS, cp.n_outer - o0));
+      T v[GROWS];
+#pragma unroll
+      for (int k = 0; k < GROWS; ++k)
+        if (k < nr) v[k] = src[(o0 + k) * cp.src_so];
+#pragma unroll
+      for (int k = 0; k < GROWS; ++k)
+        if (k < nr) store<T, FENCE>(dst + (o0 + k) * cp.dst_so, v[k]);
     }
   } else {
     const int64_t nchunks = (cp.n_inner + CHUNK - 1) / CHUNK;
@@ -102,10 +138,14 @@ void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream, const P
       const int64_t total = c.n_outer * c.n_inner;
       if (total <= 0) continue;
       const bool is_flat = c.n_inner < 64;
+      const bool is_gather = !is_flat && (c.src_si != 1 || c.dst_si != 1) && g_copy_gather;
       batch.c[batch.n] = c;
       batch.block_start[batch.n] = blocks;
       if (is_flat) batch.flat_mask |= 1u << batch.n;
-      blocks += is_flat ? (total + BLOCK - 1) / BLOCK : c.n_outer * ((c.n_inner + CHUNK - 1) / CHUNK);
+      if (is_gather) batch.gather_mask |= 1u << batch.n;
+      blocks += is_flat     ? (total + BLOCK - 1) / BLOCK
+                : is_gather ? ((c.n_inner + 63) / 64) * ((c.n_outer + 4 * GROWS - 1) / (4 * GROWS))
+                            : c.n_outer * ((c.n_inner + CHUNK - 1) / CHUNK);
       ++batch.n;
     }
     if (batch.n == 0) continue;
@@ -118,6 +158,13 @@ void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream, const P
 }
 
 }  // namespace
+
+// Gather path for strided long rows (IGG_COPY_GATHER=0: the row-chunk path,
+// for A/B measurements: benchmarks/pack_faces.py).
+bool g_copy_gather = [] {
+  const char* e = std::getenv("IGG_COPY_GATHER");
+  return !(e && e[0] == '0');
+}();
 
 template <bool FENCE>
 void launch_sized(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,

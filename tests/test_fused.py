@@ -303,3 +303,49 @@ def test_in_kernel_step_sync_counts_every_step(gpu, variant, mode, periods):
     assert b._fh.flag(0) == e0 + 5 + 9 + 1 and b._fh.flag(2) == 0
     assert torch.equal(a.T, b.T)
     igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [64, 72, 73])  # z unpack (+ 8 peel, + 1 deferred sends)
+@pytest.mark.parametrize("variant", [0, 9, 40, 42, 44])
+@pytest.mark.parametrize("periods", [(1, 1, 1), (1, 0, 1), (0, 0, 1)])
+def test_fused_z_unpack_matches_update_halo(gpu, variant, mode, periods):
+    """Send mode bit 64 (z unpack): the z faces go into the neighbours' arenas
+    (coalesced), the sweep has no z receive code and reads the z halo from the
+    field, which a copy kernel fills after the step synchronisation; bitwise
+    the same as stencil + update_halo_ (halos included after sync_halo)."""
+    a, b = _pair((34, 29, 136), periods, torch.float64, variant, mode=mode)
+    assert b.fused_mode == mode
+    a.run(9)
+    b.run(9)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,mode", [(44, 72), (14, 64), (42, 73)])
+def test_fused_z_unpack_f32_graph_loopback(gpu, variant, mode):
+    """z unpack in f32, under hipGraph replays with odd step counts and through
+    the loopback emulation's remote path."""
+    a, b = _pair((40, 36, 264), (1, 1, 1), torch.float32, variant, loopback=True, mode=mode)
+    a.run(3)
+    b.run(3)
+    b.capture(steps=4)
+    a.run(11)
+    b.run(11)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_fused_z_unpack_rejects_direct_z(gpu):
+    a, b = _pair((24, 22, 64), (1, 1, 1), torch.float64, 0, mode=64 | 4)
+    with pytest.raises(Exception, match="exclusive"):
+        b.step()
+    igg.finalize_global_grid(finalize_MPI=False)

@@ -151,6 +151,8 @@ def test_fused_forms_and_diffusion_8_ranks():
           fused(0, 5, 16, 18, 24, 6, 1, 1),
           fused(40, 8, 34, 66, 136, 5, 1, 1),
           fused(44, 4, 18, 20, 136, 4, 1, 0),
+          fused(9, 72, 18, 20, 136, 5, 0, 1),
+          fused(42, 64, 16, 18, 136, 5, 1, 1),
           f"diffusion:mgpu:24:20:18:7:0|{RCCL}",
           f"diffusion:mgpu:24:20:18:7:0|{PUT}")
 
