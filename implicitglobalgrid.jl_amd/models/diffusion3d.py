@@ -320,6 +320,14 @@ class Diffusion3D:
         self.overlap = flag
         return flag
 
+    def _overlap_streams(self) -> int:
+        """Concurrent streams of the overlapped step: the issuing stream and
+        the forked halo stream, plus the CU-masked compute stream of
+        ``reserve_cus`` on the put path (RCCL path: one side stream)."""
+        if _rccl_transport():
+            return 2
+        return 3 if self.compute_stream is not None else 2
+
     def _kw(self, variant=None, rounds=None):
         return dict(lam=self.lam, dt=self.dt, dx=self.dx, dy=self.dy, dz=self.dz,
                     variant=self.variant if variant is None else variant,
@@ -361,12 +369,13 @@ class Diffusion3D:
             self._fentry = False
             self._fstep += 1
             self._fprimed = True
-        elif self.overlap and _single_hw_queue():
-            # One hardware queue per process (GPU_MAX_HW_QUEUES=1, e.g. many
-            # ranks sharing a GPU): streams cannot run concurrently, and a
-            # hipGraph captured with the forked exchange crashed in replay
-            # (profiles/r4_overlap_crash/). Same three parts in stream order -
-            # identical results (disjoint writes), nothing lost.
+        elif self.overlap and _serial_overlap(self._overlap_streams()):
+            # Fewer hardware queues per process than concurrent streams in the
+            # overlapped step (GPU_MAX_HW_QUEUES=1, e.g. many ranks sharing a
+            # GPU): the streams cannot all run concurrently, and a hipGraph
+            # captured with the forked exchange crashed in replay with one
+            # queue (profiles/r4_overlap_crash/). Same three parts in stream
+            # order - identical results (disjoint writes), nothing lost.
             stencil.diffusion3d_(T2, T, Cp, boxes=self.slabs, **self._kw(self.halo_variant, self.halo_rounds))
             update_halo_(T2)
             stencil.diffusion3d_(T2, T, Cp, boxes=[self.interior], **self._kw(None, self.interior_rounds))
@@ -507,12 +516,24 @@ class Diffusion3D:
         return 3 * self.T.numel() * self.T.element_size()
 
 
-def _single_hw_queue() -> bool:
-    """The HIP runtime of this process uses one hardware queue
-    (GPU_MAX_HW_QUEUES=1): its streams serialise."""
-    import os
+def _hw_queues() -> int | None:
+    """Hardware queues per process of the HIP runtime (GPU_MAX_HW_QUEUES,
+    parsed as an integer: ' 01' is 1); None = the runtime's default (4)."""
+    v = os.environ.get("GPU_MAX_HW_QUEUES", "").strip()
+    try:
+        return int(v) if v else None
+    except ValueError:
+        return None
 
-    return os.environ.get("GPU_MAX_HW_QUEUES", "").strip() == "1"
+
+def _serial_overlap(streams: int) -> bool:
+    """Run the overlapped step's parts in stream order when the process has
+    fewer hardware queues than the step has concurrent streams: they could
+    not run concurrently anyway, and a captured fork in a one-queue process
+    crashed the runtime's graph replay (profiles/r4_overlap_crash/: 2 side
+    streams at GPU_MAX_HW_QUEUES=1; the full cell table is in its NOTES)."""
+    q = _hw_queues()
+    return q is not None and q < streams
 
 
 def _make_fused_halo(m: "Diffusion3D"):

@@ -196,8 +196,16 @@ def scenario_diffusion(dev, nx, ny, nz, steps, overlap):
                                                           device_type="none" if dev == "cpu" else "AMDGPU")
     gg = igg.get_global_grid()
     v = os.environ.get("IGG_TEST_VARIANT")
+    # IGG_TEST_RESERVE_CUS=k: the overlapped step's interior on a CU-masked
+    # compute stream (two forked side streams per step: the graph-fork cell
+    # that crashed the HIP runtime with one hardware queue)
     m = Diffusion3D(dtype=torch.float64, device=device, overlap=bool(int(overlap)),
-                    variant=None if v is None else int(v))
+                    variant=None if v is None else int(v),
+                    reserve_cus=int(os.environ.get("IGG_TEST_RESERVE_CUS", "0")))
+    if int(os.environ.get("IGG_TEST_RESERVE_CUS", "0")) and m.overlap:
+        from igg.parallel import halo as _H
+
+        assert m._overlap_streams() == (2 if _H.transport_name() == "rccl" else 3)
     g = int(os.environ.get("IGG_TEST_GRAPH", "0"))
     if g:
         assert m.overlap == bool(int(overlap))

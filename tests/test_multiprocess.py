@@ -123,7 +123,7 @@ def test_diffusion_gpu_multirank_put(overlap):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("queues", ["1", "4"])
+@pytest.mark.parametrize("queues", ["1", "2", "4"])
 def test_diffusion_overlap_graph_two_split_dims(queues):
     """The boundary/interior overlapped step captured in a hipGraph and
     replayed on a 2x2x1 decomposition (the N = 4 shape of a node): round 3's
@@ -132,6 +132,22 @@ def test_diffusion_overlap_graph_two_split_dims(queues):
     against the global single-array solution."""
     run_ranks(4, "diffusion", "gpu", 24, 20, 18, 7, 1,
               env_extra={**PUT_ENV, "IGG_TEST_DIMS": "2,2,1", "IGG_TEST_GRAPH": "4", "GPU_MAX_HW_QUEUES": queues},
+              timeout=160)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("queues", ["1", "4"])
+def test_diffusion_overlap_graph_two_side_streams(queues):
+    """The overlapped put step with a CU-masked compute stream forks TWO side
+    streams per step: the graph-fork cell that crashes the HIP runtime's
+    replay with one hardware queue (profiles/r4_overlap_crash/NOTES.md table:
+    2 side streams at GPU_MAX_HW_QUEUES=1 crash, every 4-queue cell replays).
+    With 4 queues the forked graph is captured and replayed; with 1 the model
+    runs the parts in stream order (models/diffusion3d.py _serial_overlap).
+    Checked against the global single-array solution."""
+    run_ranks(2, "diffusion", "gpu", 24, 20, 18, 7, 1,
+              env_extra={**PUT_ENV, "IGG_TEST_DIMS": "2,1,1", "IGG_TEST_GRAPH": "4", "GPU_MAX_HW_QUEUES": queues,
+                         "IGG_TEST_RESERVE_CUS": "8"},
               timeout=160)
 
 

@@ -79,3 +79,15 @@ def test_invalid_arguments():
     with pytest.raises(igg.IGGError):
         stencil.diffusion3d_(torch.zeros(5, 5, 5), torch.zeros(5, 5, 5), torch.zeros(5, 5, 5), lam=1, dt=1, dx=1,
                              dy=1, dz=1, boxes=[((0, 1, 1), (4, 4, 4))])
+
+
+def test_overlap_serial_rule_parses_queue_counts(monkeypatch):
+    """The overlapped step runs its parts in stream order when the process has
+    fewer hardware queues than the step has concurrent streams; the queue
+    count is parsed as an integer (' 01' is one queue)."""
+    from igg.models import diffusion3d as D
+
+    for v, streams, want in (("1", 2, True), (" 01", 2, True), ("2", 2, False), ("2", 3, True), ("4", 3, False),
+                             ("", 3, False), ("junk", 3, False)):
+        monkeypatch.setenv("GPU_MAX_HW_QUEUES", v)
+        assert D._serial_overlap(streams) is want, (v, streams)
