@@ -73,6 +73,10 @@ def main() -> int:
                     help="re-time the N fastest forms per z shape with z-edge tiles first (send mode bit 32)")
     ap.add_argument("--inkernel", type=int, default=3,
                     help="re-time the N fastest forms per shape with the in-kernel step sync (send mode bit 16)")
+    ap.add_argument("--update-halo", action="store_true",
+                    help="also time the generic path per shape: best plain stencil + update_halo_(T2) through the "
+                         "loopback emulation of exactly that shape's sides (RCCL sequential / one-phase, put)")
+    ap.add_argument("--fused", type=int, default=1, help="0: skip the fused candidates (update_halo_ column only)")
     ap.add_argument("--halo-z", type=int, default=1,
                     help="whole-line z-edge stores (DiffusionArgs::halo_z, the model's default) in plain and fused")
     a = ap.parse_args()
@@ -145,8 +149,44 @@ def main() -> int:
         base = [tuple(int(x) for x in c.split("/")) for c in a.candidates.split(",")]
     else:
         base = list(FUSED)
+    uh_forms = (("rccl", "sequential"), ("rccl", "onephase"), ("put", "auto"))
     for shape in a.shapes.split(","):
         nb = neighbours(shape)
+        if a.update_halo:
+            # generic update_halo_ of T2 after the plain stencil, through the
+            # loopback emulation of exactly these sides (one rank plays both
+            # ends of every face: the full pack -> transport -> unpack path)
+            from igg.parallel import halo as H
+            from igg.parallel.grid import global_grid
+
+            bp = best_plain.split()[1].split("/")
+            v0, r0, hz0 = int(bp[0][1:]), int(bp[1][1:]), len(bp) > 2
+            sides = [(nb[d][0] >= 0, nb[d][1] >= 0) for d in range(3)]
+            uh = {"plain": plain(v0, r0, hz0)}
+            for tr, mode in uh_forms:
+                def f_uh(tr=tr, mode=mode, k=[0]):
+                    src, dst = bufs[k[0] & 1], bufs[(k[0] + 1) & 1]
+                    native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), [n, n, n], rd2, 1e-4, eb,
+                                       inner, True, v0, s.cuda_stream, r0, hz0)
+                    H.update_halo_(dst)
+                    k[0] += 1
+                uh[f"{tr}/{mode}"] = f_uh
+            t_uh = {}
+            for tr, mode in uh_forms:  # one transport set up at a time (the engine holds one)
+                os.environ["IGG_TRANSPORT"] = tr
+                global_grid().neighbors[:, :] = -1
+                H.enable_loopback(sides)
+                H.set_halo_mode(mode)
+                r_ = bench({"plain": uh["plain"], f"{tr}/{mode}": uh[f"{tr}/{mode}"]})
+                t_uh["plain"] = min(t_uh.get("plain", float("inf")), r_.pop("plain"))
+                t_uh.update(r_)
+            tpu = t_uh.pop("plain")
+            out.setdefault("update_halo", {})[shape] = {"plain_ms": tpu, "ms": t_uh,
+                                                       "ratio": {k: v / tpu for k, v in t_uh.items()}}
+            print(f"{shape:5s} update_halo_: plain {tpu:.4f} | " +
+                  ", ".join(f"{k}={v:.4f} ({v / tpu:.4f}x)" for k, v in t_uh.items()), flush=True)
+        if not a.fused:
+            continue
         fh = native.FusedHalo(mesh, [n, n, n], eb, nb)
         fh.set_fields(T.data_ptr(), T2.data_ptr())
         cands = list(base)

@@ -328,7 +328,10 @@ _loopback_comm = None
 def enable_loopback(dims=(True, True, True)) -> None:
     """Single-GPU emulation of a rank surrounded by neighbours (perf analysis).
 
-    Every selected dimension gets both neighbours = rank 0 while the engine
+    ``dims[d]``: True (both sides), False (none) or a (low, high) pair of
+    bools - one side only emulates a node's edge/corner ranks (a 2x2x2 corner
+    rank has one neighbour per dim: ``((False, True),) * 3`` for coords 0).
+    Every selected side gets the neighbour rank 0 while the engine
     believes it is rank 1, so each face takes the full remote path — pack ->
     grouped ncclSend/ncclRecv over a 1-rank RCCL communicator (to itself) ->
     unpack (or, with IGG_TRANSPORT=put, put kernel -> own arena -> flags ->
@@ -341,16 +344,21 @@ def enable_loopback(dims=(True, True, True)) -> None:
     gg = _grid.global_grid()
     if gg.nprocs != 1 or not gg.amdgpu_enabled:
         raise IGGError("loopback mode needs a single-process grid with a GPU")
+    sides = [(bool(x[0]), bool(x[1])) if isinstance(x, (tuple, list)) else (bool(x), bool(x)) for x in dims]
     for d in range(NDIMS):
-        if dims[d]:
-            gg.neighbors[:, d] = 0
+        for s in range(2):
+            if sides[d][s]:
+                gg.neighbors[s, d] = 0
+    dims = [any(sd) for sd in sides]
     if config.transport_choice() == "put":
         _loopback_comm = native.PutTransport(native.PeerMesh(0, 1, lambda b: [bytes(b)]))
     else:
         _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
     nb = gg.neighbors.tolist()
-    peers = [0 if all(dims[d] or c == 1 for d, c in enumerate((k // 9, (k // 3) % 3, k % 3))) else PROC_NULL
-             for k in range(27)]
+    # one-phase directions (k = 9*cx + 3*cy + cz, c = 0 low / 1 none / 2 high):
+    # a peer where every non-zero component points at an emulated side
+    peers = [0 if all(c == 1 or sides[d][c // 2] for d, c in enumerate((k // 9, (k // 3) % 3, k % 3)))
+             else PROC_NULL for k in range(27)]
     peers[13] = 1
     _engine.set_grid(native.GridInfo(1, 2, gg.nxyz.tolist(), gg.overlaps.tolist(), nb, peers))
     _engine.set_transport(_loopback_comm, True)
