@@ -149,7 +149,12 @@ def main() -> int:
         base = [tuple(int(x) for x in c.split("/")) for c in a.candidates.split(",")]
     else:
         base = list(FUSED)
-    uh_forms = (("rccl", "sequential"), ("rccl", "onephase"), ("put", "auto"))
+    # one transport kind per process (parallel/halo.py enable_loopback): run
+    # the script once with IGG_TRANSPORT=rccl and once with IGG_TRANSPORT=put
+    from igg.utils import config as _cfg
+
+    uh_forms = ((("put", "auto"),) if _cfg.transport_choice() == "put"
+                else (("rccl", "sequential"), ("rccl", "onephase")))
     for shape in a.shapes.split(","):
         nb = neighbours(shape)
         if a.update_halo:
@@ -172,8 +177,10 @@ def main() -> int:
                     k[0] += 1
                 uh[f"{tr}/{mode}"] = f_uh
             t_uh = {}
-            for tr, mode in uh_forms:  # one transport set up at a time (the engine holds one)
-                os.environ["IGG_TRANSPORT"] = tr
+            for tr, mode in uh_forms:
+                if mode == "onephase" and any(sd[0] != sd[1] for sd in sides):
+                    continue  # one-sided over one self-peer: only the sequential schedule pairs (halo.py)
+                H.set_halo_mode("sequential")  # (enable_loopback refuses a one-sided RCCL loopback in one-phase mode)
                 global_grid().neighbors[:, :] = -1
                 H.enable_loopback(sides)
                 H.set_halo_mode(mode)

@@ -124,6 +124,8 @@ def set_halo_mode(mode: str) -> None:
     """Select the exchange schedule: 'sequential' (x->y->z faces, the reference
     algorithm), 'onephase' (faces+edges+corners in one phase) or 'auto'."""
     _grid.check_initialized()
+    if mode == "onephase" and _loopback_one_sided and _loopback_comm is not None and _loopback_comm.name == "rccl":
+        raise IGGError(_ONE_SIDED_ONEPHASE)
     _engine.set_mode(HALO_MODES[mode])
     _sig_modes.clear()
     for p in _plans.values():
@@ -201,7 +203,7 @@ def _set_poll_every(n: int) -> None:
 
 
 def _drop_engine() -> None:
-    global _engine, _loopback_comm
+    global _engine, _loopback_comm, _loopback_one_sided
     _release_graphs()
     _plans.clear()
     _sig_modes.clear()
@@ -209,6 +211,7 @@ def _drop_engine() -> None:
         _engine.pool_free()
     _engine = None
     _loopback_comm = None
+    _loopback_one_sided = False
     _set_dev_pending(False)
 
 
@@ -323,6 +326,17 @@ def sync_grid() -> None:
 
 
 _loopback_comm = None
+# Loopback emulation of a shape with one side in some dim (a node's edge or
+# corner rank): one process plays every neighbour through ONE self-peer, so
+# RCCL pairs messages by issue order alone. The sequential schedule issues one
+# receive and one send of equal size per emulated side; the one-phase
+# schedule's receive order (by receiver-side direction) differs from its send
+# order there, pairing messages of different sizes - a p2p receive larger than
+# its matched send reads past the send buffer (round 5: GPU memory fault in
+# benchmarks/rank_shapes.py, found on the CPU with a host loopback transport).
+_loopback_one_sided = False
+_ONE_SIDED_ONEPHASE = ("loopback emulation of a one-sided shape: the one-phase schedule cannot pair its messages "
+                       "through one self-peer over RCCL; use the sequential schedule (or the put transport)")
 
 
 def enable_loopback(dims=(True, True, True)) -> None:
@@ -340,7 +354,7 @@ def enable_loopback(dims=(True, True, True)) -> None:
     too, so apps enable their boundary/interior overlap. Results equal a
     periodic exchange.
     """
-    global _loopback_comm
+    global _loopback_comm, _loopback_one_sided
     gg = _grid.global_grid()
     if gg.nprocs != 1 or not gg.amdgpu_enabled:
         raise IGGError("loopback mode needs a single-process grid with a GPU")
@@ -350,10 +364,20 @@ def enable_loopback(dims=(True, True, True)) -> None:
             if sides[d][s]:
                 gg.neighbors[s, d] = 0
     dims = [any(sd) for sd in sides]
-    if config.transport_choice() == "put":
-        _loopback_comm = native.PutTransport(native.PeerMesh(0, 1, lambda b: [bytes(b)]))
-    else:
-        _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
+    _loopback_one_sided = any(sd[0] != sd[1] for sd in sides)
+    want = "put" if config.transport_choice() == "put" else "rccl"
+    # A later call (another emulated shape) reuses the loopback transport of
+    # the same kind instead of replacing it: a replaced RCCL communicator or
+    # put mesh is destroyed mid-process, and a put -> RCCL switch that way was
+    # followed by a GPU memory fault (round 5, benchmarks/rank_shapes.py).
+    if _loopback_comm is None or _loopback_comm.name != want:
+        if _loopback_comm is not None:
+            raise IGGError(f"loopback mode: the '{_loopback_comm.name}' loopback transport exists; one transport "
+                           f"kind per process (IGG_TRANSPORT={want} requested)")
+        if want == "put":
+            _loopback_comm = native.PutTransport(native.PeerMesh(0, 1, lambda b: [bytes(b)]))
+        else:
+            _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
     nb = gg.neighbors.tolist()
     # one-phase directions (k = 9*cx + 3*cy + cz, c = 0 low / 1 none / 2 high):
     # a peer where every non-zero component points at an emulated side
@@ -362,6 +386,8 @@ def enable_loopback(dims=(True, True, True)) -> None:
     peers[13] = 1
     _engine.set_grid(native.GridInfo(1, 2, gg.nxyz.tolist(), gg.overlaps.tolist(), nb, peers))
     _engine.set_transport(_loopback_comm, True)
+    if _loopback_one_sided and want == "rccl" and _engine.mode == HALO_MODES["onephase"]:
+        raise IGGError(_ONE_SIDED_ONEPHASE)
     _plans.clear()
     _sig_modes.clear()
 
@@ -456,6 +482,12 @@ def _remote_peers() -> bool:
 
 
 def _tune_mode(fs, stream: int) -> int:
+    if _loopback_one_sided and _loopback_comm is not None and _loopback_comm.name == "rccl":
+        return HALO_MODES["sequential"]  # the only schedule a one-sided RCCL loopback can pair
+    return _tune_mode_timed(fs, stream)
+
+
+def _tune_mode_timed(fs, stream: int) -> int:
     """Time the sequential and one-phase schedules on this field set (MAX over
     ranks, so every rank picks the same winner) and return the faster mode.
     Collective like update_halo_ itself. Safe to run on live data: a halo
