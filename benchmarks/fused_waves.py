@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--shape", default="xyz",
+                    help="neighbour sides of the exchanging halo (rank_shapes.py names: xyz = 6 faces, "
+                         "xyz+ = a 2x2x2 corner rank with coords 0, ...)")
     a = ap.parse_args()
     n = a.n
     igg.init_global_grid(n, n, n, periodx=1, periody=1, periodz=1, quiet=True)
@@ -48,7 +51,10 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     inner = [([1, 1, 1], [n - 1, n - 1, n - 1])]
     mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
-    fh6 = native.FusedHalo(mesh, [n, n, n], eb, [[0, 0], [0, 0], [0, 0]])
+    dims = a.shape.rstrip("+-")
+    side = a.shape[len(dims):] or "+-"
+    nb = [[0 if (d in dims and "-" in side) else -1, 0 if (d in dims and "+" in side) else -1] for d in "xyz"]
+    fh6 = native.FusedHalo(mesh, [n, n, n], eb, nb)
     # its own mesh: a neighbourless halo advances EPOCH without publishing
     # ARRIVED, which would stall fh6's in-kernel step sync on a shared flag block
     fh0 = native.FusedHalo(native.PeerMesh(0, 1, lambda b: [bytes(b)]), [n, n, n], eb,
@@ -75,7 +81,8 @@ def main():
             ts.append(e0.elapsed_time(e1) / a.reps)
         return sorted(ts)[1]
 
-    print(f"n={n}^3 {a.dtype} rounds={a.rounds} mode={a.mode}: ms per step (stencil + sync), per-class wave stats in us")
+    print(f"n={n}^3 {a.dtype} rounds={a.rounds} mode={a.mode} shape={a.shape} (nb {nb}): ms per step (stencil + "
+          f"sync), per-class wave stats in us")
     for v in (int(x) for x in a.variants.split(",")):
         pv = PLAIN_OF.get(v, v)
         tp = ev_time(lambda: native.diffusion3d(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), [n, n, n], rd2, 1e-4,

@@ -77,9 +77,14 @@ def main() -> int:
                     help="also time the generic path per shape: best plain stencil + update_halo_(T2) through the "
                          "loopback emulation of exactly that shape's sides (RCCL sequential / one-phase, put)")
     ap.add_argument("--fused", type=int, default=1, help="0: skip the fused candidates (update_halo_ column only)")
+    ap.add_argument("--graph", action="store_true",
+                    help="time hipGraph replays of --steps captured steps (the bench's timed form) instead of eager "
+                         "launches (--steps must be even)")
     ap.add_argument("--halo-z", type=int, default=1,
                     help="whole-line z-edge stores (DiffusionArgs::halo_z, the model's default) in plain and fused")
     a = ap.parse_args()
+    if a.graph and a.steps % 2:
+        raise SystemExit("--graph: --steps must be even (the ping-pong buffers return to their roles)")
     n = a.n
     hz = bool(a.halo_z)
     dt = getattr(torch, a.dtype)
@@ -125,13 +130,29 @@ def main() -> int:
         for f in fns.values():
             for _ in range(2):
                 f()
+        runs = dict(fns)
+        if a.graph:
+            # the steps as the bench's timed region runs them: hipGraph
+            # replays (launch gaps of the sync / unpack kernels as in a run)
+            runs = {}
+            for c, f in fns.items():
+                g = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize()
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(a.steps):
+                        f()
+                torch.cuda.synchronize()
+                runs[c] = g
         times = {c: [] for c in fns}
         for _ in range(a.rounds):
-            for c, f in fns.items():
+            for c, f in runs.items():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-                for _ in range(a.steps):
-                    f()
+                if a.graph:
+                    f.replay()
+                else:
+                    for _ in range(a.steps):
+                        f()
                 e1.record(s)
                 e1.synchronize()
                 times[c].append(e0.elapsed_time(e1) / a.steps)
