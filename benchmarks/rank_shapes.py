@@ -101,6 +101,8 @@ def main() -> int:
     Cp.copy_(torch.rand(n, n, n, generator=g, dtype=torch.float64).to(dt) + 1)
     rd2 = [1.0, 1.0, 1.0]
     eb = T.element_size()
+    if a.graph:  # captures need a non-default stream; every launch below goes to it
+        torch.cuda.set_stream(torch.cuda.Stream())
     s = torch.cuda.current_stream()
     inner = [([1, 1, 1], [n - 1, n - 1, n - 1])]
     mesh = native.PeerMesh(0, 1, lambda b: [bytes(b)])
