@@ -971,8 +971,7 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
                    and model._fh.in_kernel_sync_for(16) and not model._fh.in_kernel_sync_for(0)
                    and os.environ.get("IGG_FUSED_INKERNEL", "1") != "0")
     if diffusion and _max_over_ranks(comm, 0.0 if inkernel_ok else 1.0) == 0.0:
-        # (the z-unpack forms, bit 64, always use the sync kernel: no in-kernel twin)
-        front = [c for c, _t in sorted(times.items(), key=lambda kv: kv[1]) if not c[1] & (16 | 64)][:2]
+        front = [c for c, _t in sorted(times.items(), key=lambda kv: kv[1]) if not c[1] & 16][:2]
         timing_passes([(v, fm | 16, gr) for v, fm, gr in front])
     model.set_fused(False)
     model.graph = None

@@ -249,9 +249,7 @@ def main() -> int:
             for k, v_ in to.items():
                 t[k] = min(t.get(k, float("inf")), v_)
         if a.inkernel > 0:  # the fastest forms again with the step sync inside the kernel
-            # (z unpack, bit 64, always uses the sync kernel: no in-kernel form)
-            front = sorted((c for c in t if c != "plain" and not int(c.split("/")[1][1:]) & 64),
-                           key=t.get)[:a.inkernel]
+            front = sorted((c for c in t if c != "plain"), key=t.get)[:a.inkernel]
             fk = {}
             for c in front:
                 v, m, r = (int(x[1:]) for x in c.split("/"))

@@ -111,7 +111,7 @@ HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z,
   return io;
 }
 
-void FusedHalo::unpack_z(int64_t step, uintptr_t t2, hipStream_t stream) const {
+void FusedHalo::unpack_z(int64_t step, uintptr_t t2, hipStream_t stream, bool wait) const {
   // My arena half (step & 1) holds, at region off_[2][s], the z plane the
   // neighbour at side s computed in its step `step` (layout x*zp + (y-1),
   // x in [1, n0-2], y in [1, n1-2]): my z halo at side s (z = 0 / n2-1) of
@@ -133,7 +133,21 @@ void FusedHalo::unpack_z(int64_t step, uintptr_t t2, hipStream_t stream) const {
     c.dst_si = n2;
     cs.push_back(c);
   }
-  launch_copy2d(cs, static_cast<int>(eb), stream);
+  CopyWait w;
+  if (wait) {
+    // in-kernel step sync: no sync kernel ran since the stencil, whose last
+    // exchanging wave advanced EPOCH; the z senders' ARRIVED for that step
+    // orders this unpack after their sends (docs/COHERENCE.md, z unpack)
+    w.flags = sync_.my_flags;
+    w.timeout_ticks = sync_.timeout_ticks;
+    for (int s = 0; s < 2; ++s) {
+      const int r = nb_[2][s];
+      if (r == PROC_NULL) continue;
+      if (w.n == 1 && w.rank[0] == r) continue;  // both z sides one peer (dims 2, periodic)
+      w.rank[w.n++] = r;
+    }
+  }
+  launch_copy2d(cs, static_cast<int>(eb), stream, false, ParityShift{}, w);
 }
 
 void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step, bool primed,
@@ -153,9 +167,9 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
   // rank's kernel needs: the forced 8-rank shared-GPU rehearsal timed out).
   // IGG_FUSED_SYNC_KERNEL / set_step_sync override both.
   bool used = false;
-  // (z unpack: the unpack must follow the step's synchronisation, so the
-  // sync-kernel form always)
-  if (!zu && in_kernel_sync(mode) && sync_.n_out > 0) {  // no neighbour: nothing to synchronise in the kernel
+  // (z unpack with the in-kernel form: the unpack kernel itself waits for the
+  // z senders' ARRIVED of this step before it reads the arena)
+  if (in_kernel_sync(mode) && sync_.n_out > 0) {  // no neighbour: nothing to synchronise in the kernel
     x.sync = step_sync_from(sync_);
     x.sync_used = &used;
   }
@@ -164,7 +178,7 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
   const int kmode = (mode & ~(IN_KERNEL_SYNC | Z_UNPACK)) | (zu ? 4 : 0);
   launch_diffusion3d_fused(a, x, variant, kmode, stream);
   if (!used) sync(stream);
-  if (zu) unpack_z(step, a.t2, stream);
+  if (zu) unpack_z(step, a.t2, stream, used);
   open_ = used;
 }
 

@@ -27,6 +27,18 @@ struct Copy2D {
   int64_t dst_so, dst_si;
 };
 
+// Optional wait at the start of a copy launch (the z unpack of FusedHalo with
+// the in-kernel step synchronisation: no sync kernel runs between the stencil
+// and the unpack): one thread per workgroup spins until ARRIVED[rank] >= EPOCH
+// in `flags` (this GPU's flag block, put.hpp) for every listed rank, then a
+// system acquire orders the workgroup's loads after the senders' stores.
+struct CopyWait {
+  uint64_t* flags = nullptr;  // own flag block (EPOCH, ERROR, ARRIVED[])
+  int rank[2] = {0, 0};
+  int n = 0;
+  int64_t timeout_ticks = 0;
+};
+
 constexpr int MAX_BATCH = 32;  // all 26 one-phase directions in one launch; kernarg < 4 KiB
 
 struct CopyBatch {
@@ -41,6 +53,7 @@ struct CopyBatch {
   int64_t parity_bytes = 0;
   int parity_side = 0;
   int parity_add = 0;  // half = ((*epoch + parity_add) & 1)
+  CopyWait wait;       // n > 0: wait for the senders' arrival first
 };
 
 struct ParityShift {
@@ -56,7 +69,8 @@ struct ParityShift {
 // fine-grained arena reach the owner before the following sync kernel
 // publishes them; docs/COHERENCE.md).
 void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
-                   bool system_fence = false, const ParityShift& parity = ParityShift{});
+                   bool system_fence = false, const ParityShift& parity = ParityShift{},
+                   const CopyWait& wait = CopyWait{});
 
 // Host: perform all copies now (threaded above THREADCOPY_THRESHOLD bytes).
 void host_copy2d(const std::vector<Copy2D>& copies, int elem_bytes);

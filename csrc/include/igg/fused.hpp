@@ -107,11 +107,13 @@ class FusedHalo {
   // received halo, no scattered 8-B remote stores as with direct z), and after
   // the sync kernel a copy kernel writes the received z faces (my arena, this
   // step's half) into t2's z halo column, which the next sweep reads like any
-  // other element. Needs the sync-kernel form (bit 16 is ignored with it) and
-  // excludes direct z (bit 4).
+  // other element. Excludes direct z (bit 4). With the in-kernel step sync
+  // (bit 16) the unpack kernel waits for the z senders' ARRIVED flags itself
+  // (no sync kernel runs between the stencil and the unpack).
   static constexpr int Z_UNPACK = 64;
-  // The unpack of the z-unpack form (after the step synchronisation of `step`).
-  void unpack_z(int64_t step, uintptr_t t2, hipStream_t stream) const;
+  // The unpack of the z-unpack form (after the step synchronisation of `step`;
+  // `wait`: the in-kernel form, the unpack first waits for the z senders).
+  void unpack_z(int64_t step, uintptr_t t2, hipStream_t stream, bool wait = false) const;
   // Whether a step with send mode `mode` synchronises inside the kernel.
   bool in_kernel_sync(int mode = 0) const;
 

@@ -12,6 +12,7 @@
 #include <cstdlib>
 
 #include "igg/copy.hpp"
+#include "igg/devsync.hpp"
 #include "igg/sysstore.hpp"
 
 namespace igg {
@@ -50,6 +51,18 @@ __device__ __forceinline__ void store(T* p, const T& v) {
 template <typename T, bool FENCE>
 __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch batch) {
   const int64_t b = blockIdx.x;
+  if (batch.wait.n > 0) {
+    // (CopyWait) the senders' data of the step this GPU has just completed
+    // (EPOCH) must have arrived: their ARRIVED flags publish it
+    if (threadIdx.x == 0) {
+      const uint64_t e = load_sys_relaxed(batch.wait.flags + PutFlags::EPOCH);
+      for (int k = 0; k < batch.wait.n; ++k)
+        spin_geq(batch.wait.flags + PutFlags::ARRIVED + batch.wait.rank[k], e, batch.wait.flags,
+                 batch.wait.timeout_ticks, 0x400 + k);
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
   int c = 0;
   // Wave-uniform scan over <= MAX_BATCH prefix sums (scalar loads from kernarg).
   while (c + 1 < batch.n && b >= batch.block_start[c + 1]) ++c;
@@ -123,7 +136,8 @@ __global__ void __launch_bounds__(BLOCK) copy2d_batch_kernel(const CopyBatch bat
 }
 
 template <typename T, bool FENCE>
-void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream, const ParityShift& par) {
+void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream, const ParityShift& par,
+                  const CopyWait& wait) {
   size_t pos = 0;
   while (pos < copies.size()) {
     CopyBatch batch{};
@@ -132,6 +146,7 @@ void launch_typed(const std::vector<Copy2D>& copies, hipStream_t stream, const P
     batch.parity_bytes = par.bytes;
     batch.parity_side = par.side;
     batch.parity_add = par.add;
+    batch.wait = wait;
     int64_t blocks = 0;
     while (pos < copies.size() && batch.n < MAX_BATCH) {
       const Copy2D& c = copies[pos++];
@@ -168,22 +183,23 @@ bool g_copy_gather = [] {
 
 template <bool FENCE>
 void launch_sized(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
-                  const ParityShift& par) {
+                  const ParityShift& par, const CopyWait& wait) {
   switch (elem_bytes) {
-    case 1: launch_typed<uint8_t, FENCE>(copies, stream, par); break;
-    case 2: launch_typed<uint16_t, FENCE>(copies, stream, par); break;
-    case 4: launch_typed<uint32_t, FENCE>(copies, stream, par); break;
-    case 8: launch_typed<uint64_t, FENCE>(copies, stream, par); break;
-    case 16: launch_typed<B16, FENCE>(copies, stream, par); break;
+    case 1: launch_typed<uint8_t, FENCE>(copies, stream, par, wait); break;
+    case 2: launch_typed<uint16_t, FENCE>(copies, stream, par, wait); break;
+    case 4: launch_typed<uint32_t, FENCE>(copies, stream, par, wait); break;
+    case 8: launch_typed<uint64_t, FENCE>(copies, stream, par, wait); break;
+    case 16: launch_typed<B16, FENCE>(copies, stream, par, wait); break;
     default: fail("launch_copy2d: unsupported element size ", elem_bytes, " bytes");
   }
 }
 
 void launch_copy2d(const std::vector<Copy2D>& copies, int elem_bytes, hipStream_t stream,
-                   bool system_fence, const ParityShift& parity) {
+                   bool system_fence, const ParityShift& parity, const CopyWait& wait) {
   if (copies.empty()) return;
-  if (system_fence) launch_sized<true>(copies, elem_bytes, stream, parity);
-  else launch_sized<false>(copies, elem_bytes, stream, parity);
+  if (wait.n < 0 || wait.n > 2 || (wait.n > 0 && !wait.flags)) fail("launch_copy2d: invalid CopyWait");
+  if (system_fence) launch_sized<true>(copies, elem_bytes, stream, parity, wait);
+  else launch_sized<false>(copies, elem_bytes, stream, parity, wait);
 }
 
 }  // namespace igg

@@ -279,7 +279,7 @@ def test_graph_after_odd_step_counts(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,mode", [(0, 0), (0, 1), (40, 8), (42, 4), (42, 12), (50, 1)])
+@pytest.mark.parametrize("variant,mode", [(0, 0), (0, 1), (40, 8), (42, 4), (42, 12), (50, 1), (40, 72)])
 @pytest.mark.parametrize("periods", [(1, 1, 1), (0, 1, 0), (1, 0, 1)])
 def test_in_kernel_step_sync_counts_every_step(gpu, variant, mode, periods):
     """The in-kernel step synchronisation advances EPOCH exactly once per step
@@ -318,6 +318,28 @@ def test_fused_z_unpack_matches_update_halo(gpu, variant, mode, periods):
     assert b.fused_mode == mode
     a.run(9)
     b.run(9)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [80, 88])  # z unpack + in-kernel step sync (+ 8 peel)
+@pytest.mark.parametrize("variant", [0, 9, 40, 42])
+@pytest.mark.parametrize("periods", [(1, 1, 1), (0, 0, 1)])
+def test_fused_z_unpack_in_kernel_sync_matches_update_halo(gpu, variant, mode, periods):
+    """z unpack with the step synchronisation inside the fused kernel: no sync
+    kernel runs, the unpack kernel waits for the z senders' ARRIVED flags
+    itself (CopyWait); eager steps and graph replays, bitwise."""
+    a, b = _pair((34, 29, 136), periods, torch.float64, variant, mode=mode)
+    assert b._fh.in_kernel_sync_for(b.fused_mode)
+    a.run(3)
+    b.run(3)
+    b.capture(steps=4)
+    a.run(8)
+    b.run(8)
     b.sync_halo()
     torch.cuda.synchronize()
     b.check()

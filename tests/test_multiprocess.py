@@ -248,7 +248,10 @@ def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
 @pytest.mark.gpu
 @pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 1, 0), ("0", "0")),
                                                (4, (20, 22, 32, 5, 1, 1), ("0", "1")),
-                                               (8, (18, 20, 40, 7, 1, 0), ("0", "5"))])
+                                               (8, (18, 20, 40, 7, 1, 0), ("0", "5")),
+                                               # z unpack: the unpack kernel waits for the z senders itself
+                                               (8, (18, 20, 136, 5, 0, 0), ("0", "72")),
+                                               (2, (24, 20, 64, 6, 0, 1), ("0", "64"))])
 def test_diffusion_gpu_multirank_fused_in_kernel_sync(nprocs, cfg, kernel):
     """The step synchronisation inside the fused kernel across processes
     (forced: ranks sharing one GPU default to the sync kernel, because waiting
