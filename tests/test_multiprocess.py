@@ -255,11 +255,7 @@ def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
                                                # z unpack: the unpack kernel waits for the z senders itself
                                                (8, (18, 20, 136, 5, 0, 0), ("0", "72")),
                                                (2, (24, 20, 64, 6, 0, 1), ("0", "64")),
-                                               # in-kernel z unpack + in-kernel step sync: 2 ranks only (8
-                                               # ranks on ONE GPU starve each other's kernels with spinning
-                                               # waves: a 20 s wait timed out, profiles/r5_shapes/ pass 6;
-                                               # never the library's choice on a shared GPU)
-                                               (2, (24, 20, 136, 6, 0, 1), ("0", "136"))])
+                                               (8, (18, 20, 136, 5, 0, 0), ("0", "136"))])
 def test_diffusion_gpu_multirank_fused_in_kernel_sync(nprocs, cfg, kernel):
     """The step synchronisation inside the fused kernel across processes
     (forced: ranks sharing one GPU default to the sync kernel, because waiting
