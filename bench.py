@@ -79,11 +79,6 @@ FUSED_DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4), (44, 36, 4))
 # neighbour only (without one these equal their mode & ~64 forms).
 FUSED_ZUNPACK = ((9, 64, 3), (42, 64, 2), (40, 64, 2), (0, 64, 3))
 FUSED_ZUNPACK_F32 = ((44, 64, 4), (14, 64, 3))
-# In-kernel z unpack (send mode bit 128, FusedHalo::Z_UNPACK_IN_KERNEL): the
-# same, with the unpack done by extra workgroups at the front of the next
-# step's stencil launch (no unpack kernel).
-FUSED_ZUNPACK_K = ((40, 128, 2), (9, 128, 2), (42, 128, 2), (0, 128, 3))
-FUSED_ZUNPACK_K_F32 = ((0, 128, 3), (14, 128, 3))
 # (send mode bit 32 = z-edge tiles dispatched first: the f32 2x2x2 corner's best
 # form at 4 grid rounds; slower for f64 at every round count, profiles/r4_shapes/)
 # Win record of the fused forms (rounds 2-4: the bench's A/Bs on every box and
@@ -897,9 +892,9 @@ def select_fused(model, comm, log, mode: str, graph: bool = True) -> dict | None
             if model.T.dtype.itemsize == 4:
                 cands += FUSED_DIRECT_F32
         if any(model.sides[2]):
-            cands += FUSED_ZUNPACK + FUSED_ZUNPACK_K
+            cands += FUSED_ZUNPACK
             if model.T.dtype.itemsize == 4:
-                cands += FUSED_ZUNPACK_F32 + FUSED_ZUNPACK_K_F32
+                cands += FUSED_ZUNPACK_F32
         # every form also with its exchanged x planes peeled off the chunk sweep
         # (send mode bit 8: profiles/r2_peel/, -1.8 % f64 / -2.8 % f32 interior rank)
         cands += [(v, fm | 8, gr) for v, fm, gr in cands]

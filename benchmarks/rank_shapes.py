@@ -43,8 +43,8 @@ DIRECT = ((40, 4, 2), (42, 4, 2), (42, 5, 2), (50, 4, 2), (0, 4, 3))
 DIRECT_F32 = ((44, 4, 3), (44, 4, 4), (14, 4, 4))
 # z unpack (send mode bit 64, FusedHalo::Z_UNPACK): arena z sends, no z receive
 # in the sweep, a copy kernel writes the received z faces after the step sync
-ZUNPACK = ((9, 64, 3), (42, 64, 2), (40, 64, 2), (0, 64, 3), (40, 128, 2), (9, 128, 2), (42, 128, 2), (0, 128, 3))
-ZUNPACK_F32 = ((44, 64, 4), (14, 64, 3), (0, 128, 3), (14, 128, 3))
+ZUNPACK = ((9, 64, 3), (42, 64, 2), (40, 64, 2), (0, 64, 3))
+ZUNPACK_F32 = ((44, 64, 4), (14, 64, 3))
 
 
 def neighbours(shape: str):

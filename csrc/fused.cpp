@@ -65,8 +65,7 @@ void FusedHalo::set_fields(uintptr_t a, uintptr_t b) {
   fields_ = mesh_->map_buffers({a, b});  // collective
 }
 
-HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z, bool z_unpack,
-                         bool z_unpack_in_kernel) const {
+HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z, bool z_unpack) const {
   HaloIOArgs io{};
   const int64_t eb = elem_;
   const int64_t wh = (step & 1) * half_, rh = ((step + 1) & 1) * half_;
@@ -84,21 +83,7 @@ HaloIOArgs FusedHalo::io(int64_t step, bool primed, uintptr_t t2, bool direct_z,
   // where nobody else writes t2's z halo column during the kernel.
   for (int s = 0; s < 2; ++s) io.zh[s] = 1;
   io.z_out_arena = true;
-  if ((direct_z ? 1 : 0) + (z_unpack ? 1 : 0) + (z_unpack_in_kernel ? 1 : 0) > 1)
-    fail("FusedHalo: direct z, z unpack and in-kernel z unpack are exclusive send modes");
-  if (z_unpack_in_kernel) {
-    // in[2] (this step's received z regions, set above when primed) feed the
-    // unpack workgroups of the launch; the sweep itself reads no z arena
-    io.uz = true;
-    io.uz_flags = sync_.my_flags;
-    io.uz_timeout = sync_.timeout_ticks;
-    for (int s = 0; s < 2; ++s) {
-      const int r = nb_[2][s];
-      if (r == PROC_NULL) continue;
-      if (io.uz_nrank == 1 && io.uz_rank[0] == r) continue;
-      io.uz_rank[io.uz_nrank++] = r;
-    }
-  }
+  if (direct_z && z_unpack) fail("FusedHalo: direct z and z unpack are exclusive send modes");
   if (z_unpack)
     for (int s = 0; s < 2; ++s) io.in[2][s] = 0;  // the z halo comes from the field (unpack_z of the last step)
   if (direct_z && (nb_[2][0] != PROC_NULL || nb_[2][1] != PROC_NULL)) {
@@ -171,12 +156,9 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
     if (a.n[d] != n_[d]) fail("FusedHalo.step: field shape does not match the fused halo's local grid");
   if (a.elem_bytes != elem_) fail("FusedHalo.step: field dtype does not match the fused halo");
   if (entry) sync(stream);  // entry barrier (fused.hpp)
-  const bool has_z = nb_[2][0] != PROC_NULL || nb_[2][1] != PROC_NULL;
-  const bool zu = (mode & Z_UNPACK) != 0 && has_z;
-  const bool zk = (mode & Z_UNPACK_IN_KERNEL) != 0 && has_z;
-  if ((zu || zk) && (mode & 4)) fail("FusedHalo.step: send mode bits 4 (direct z) and 64/128 (z unpack) are exclusive");
-  if (zu && zk) fail("FusedHalo.step: send mode bits 64 and 128 (z unpack forms) are exclusive");
-  HaloIOArgs x = io(step, primed, a.t2, (mode & 4) != 0, zu, zk);
+  const bool zu = (mode & Z_UNPACK) != 0 && (nb_[2][0] != PROC_NULL || nb_[2][1] != PROC_NULL);
+  if (zu && (mode & 4)) fail("FusedHalo.step: send mode bits 4 (direct z) and 64 (z unpack) are exclusive");
+  HaloIOArgs x = io(step, primed, a.t2, (mode & 4) != 0, zu);
   // Step synchronisation: the 1-wave sync kernel after the stencil (default:
   // rehearsed with 8 ranks, and as fast as the in-kernel form,
   // profiles/r3_boxes/), or inside the kernel (put.hpp StepSync) with send
@@ -191,12 +173,9 @@ void FusedHalo::step(const DiffusionArgs& a, int variant, int mode, int64_t step
     x.sync = step_sync_from(sync_);
     x.sync_used = &used;
   }
-  // with the in-kernel step sync the unpack workgroups first wait for the z
-  // senders' arrival (no sync kernel ran since their step)
-  x.uz_wait_arrival = zk && x.sync.my_flags != nullptr;
   // the kernel form: z unpack = the no-z-receive form (bit 4's kernel) with
   // the z sends into the arena (x.out[2], zrow 1)
-  const int kmode = (mode & ~(IN_KERNEL_SYNC | Z_UNPACK | Z_UNPACK_IN_KERNEL)) | ((zu || zk) ? 4 : 0);
+  const int kmode = (mode & ~(IN_KERNEL_SYNC | Z_UNPACK)) | (zu ? 4 : 0);
   launch_diffusion3d_fused(a, x, variant, kmode, stream);
   if (!used) sync(stream);
   if (zu) unpack_z(step, a.t2, stream, used);

@@ -67,8 +67,7 @@ class FusedHalo {
   // neighbours' arenas (whole-line coalesced stores) and nothing is read from
   // the arena along z in the kernel: unpack_z() writes the received z faces
   // into t2's halo column after the step synchronisation.
-  HaloIOArgs io(int64_t step, bool primed, uintptr_t t2 = 0, bool direct_z = false, bool z_unpack = false,
-                bool z_unpack_in_kernel = false) const;
+  HaloIOArgs io(int64_t step, bool primed, uintptr_t t2 = 0, bool direct_z = false, bool z_unpack = false) const;
   // Collective: the two ping-pong field buffers of this rank (same order on
   // every rank, registered at the same step); needed by direct z (mode bit 4).
   // Every rank swaps them in lockstep, so "my t2 is buffer k" means "each
@@ -112,13 +111,6 @@ class FusedHalo {
   // (bit 16) the unpack kernel waits for the z senders' ARRIVED flags itself
   // (no sync kernel runs between the stencil and the unpack).
   static constexpr int Z_UNPACK = 64;
-  // Send mode bit of the in-kernel z unpack: as Z_UNPACK, but the received z
-  // faces of the previous step are copied into the field's z halo columns by
-  // extra workgroups at the front of THIS step's stencil launch (dispatched
-  // first); the z-edge waves wait for them (a flag word, put.hpp UEPOCH) and
-  // read the halo from the field. No unpack kernel; works with the sync
-  // kernel and with the in-kernel step sync. Excludes bits 4 and 64.
-  static constexpr int Z_UNPACK_IN_KERNEL = 128;
   // The unpack of the z-unpack form (after the step synchronisation of `step`;
   // `wait`: the in-kernel form, the unpack first waits for the z senders).
   void unpack_z(int64_t step, uintptr_t t2, hipStream_t stream, bool wait = false) const;

@@ -22,7 +22,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <vector>
 
 #include "igg/devmath.hpp"
@@ -107,16 +106,6 @@ struct HxScal {
   // one full-line store (launch_hx decides per side).
   int zh_lo, zh_hi;
   StepSync sync;  // in-kernel step synchronisation (put.hpp; my_flags null: a sync kernel follows)
-  // In-kernel z unpack (send mode bit 128, FusedHalo): the first uz_blocks
-  // workgroups of the grid copy the received z faces (zi0/zi1: this step's
-  // arena regions) into t's z halo columns, then publish UEPOCH; the z-edge
-  // waves of the sweep wait for it and read the halo from the field (FEAT 203
-  // sweep: no z receive code). uz_blocks 0: off. uz_flags: own flag block.
-  int64_t uz_blocks;
-  uint64_t* uz_flags;
-  int uz_wait_arrival;  // with the in-kernel step sync: wait for the z senders' ARRIVED first
-  int uz_rank[2], uz_nrank;
-  int64_t uz_timeout;  // wall_clock64 ticks of the bounded spins
 };
 
 // Tile (z tile, y tile, x chunk) of block `bid` of `nblk`. Default: z tiles
@@ -212,11 +201,11 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   // instead of at the kernel's tail. Scheduling only: results are unchanged.
   // (hx_tile; send mode bit 32 also puts the z-edge tiles first.)
   const int64_t nch = (a.n0 - 2 + a.ch - 1) / a.ch;
-  const HxTile<T> tile = hx_tile(a, blockIdx.x - a.uz_blocks, gridDim.x - a.uz_blocks);
+  const HxTile<T> tile = hx_tile(a, blockIdx.x, gridDim.x);
   const int64_t tz = tile.tz, ty = tile.ty;
   int64_t cx = tile.cx;
   if constexpr (RV) {  // reversed march (probe form): chunks from the top, default order
-    const int64_t b = xcd_remap(blockIdx.x - a.uz_blocks, gridDim.x - a.uz_blocks);
+    const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
     cx = nch - 1 - (b / a.ntz) / a.nty;
   }
   const int lane = threadIdx.x & 63;
@@ -588,65 +577,6 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   if (remote) __builtin_amdgcn_s_waitcnt(0);
 }
 
-// In-kernel z unpack (HxScal::uz_blocks): workgroups [0, uz_blocks) of the
-// grid copy this step's received z faces (arena regions zi0 / zi1, layout
-// x*zp + (y-1)) into t's z halo columns (z = 0 / n2-1) for x in [1, n0-2],
-// y in [1, n1-2] - the only halo elements a sweep reads, each read only by
-// the z-edge wave that owns its row. The last workgroup to finish publishes
-// UEPOCH = EPOCH + 1 (EPOCH does not change while this kernel's z-edge waves
-// wait: the sync kernel runs after it, and with the in-kernel step sync the
-// last exchanging wave advances it only after every z-edge wave retired).
-// Dispatched first (lowest block ids), they are resident before any waiting
-// wave; t is written through a const-cast pointer: no thread that reads t
-// reads these elements before the UEPOCH acquire (hx_unpack_wait).
-template <typename T>
-__device__ void hx_unpack_z(const T* t, const T* zi0, const T* zi1, const HxScal<T>& a) {
-  const int tid = threadIdx.x;
-  const int nthreads = blockDim.x;
-  uint64_t* fl = a.uz_flags;
-  const uint64_t c = load_sys_relaxed(fl + PutFlags::EPOCH);
-  if (a.uz_wait_arrival) {
-    // in-kernel step sync: the senders' step c data must have arrived
-    if (tid < a.uz_nrank)
-      spin_geq(fl + PutFlags::ARRIVED + a.uz_rank[tid], c, fl, a.uz_timeout, 0x500 + tid);
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  }
-  const int64_t n1 = a.n1, n2 = a.n2, m1 = n1 - 2;
-  const int64_t per = (a.n0 - 2) * m1;
-  T* tw = const_cast<T*>(t);
-  for (int sd = 0; sd < 2; ++sd) {
-    const T* src = sd == 0 ? zi0 : zi1;
-    if (!src) continue;
-    const int64_t col = sd == 0 ? 0 : n2 - 1;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * nthreads + tid; i < per; i += a.uz_blocks * nthreads) {
-      const int64_t x = 1 + i / m1, y = 1 + (i - (i / m1) * m1);
-      tw[(x * n1 + y) * n2 + col] = src[x * a.zp + (y - 1)];
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint64_t old =
-        __hip_atomic_fetch_add(fl + PutFlags::UCOUNT, uint64_t{1}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == static_cast<uint64_t>(a.uz_blocks)) {
-      __hip_atomic_store(fl + PutFlags::UCOUNT, uint64_t{0}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(fl + PutFlags::UEPOCH, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// A z-edge wave of the in-kernel z unpack: wait until UEPOCH > EPOCH, then
-// an agent-scope acquire (the unpack workgroups ran on this GPU).
-template <typename T>
-__device__ void hx_unpack_wait(const HxScal<T>& a) {
-  uint64_t* fl = a.uz_flags;
-  const uint64_t c = load_sys_relaxed(fl + PutFlags::EPOCH);
-  spin_geq(fl + PutFlags::UEPOCH, c + 1, fl, a.uz_timeout, 0x600);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
 // The kernel: each wave runs the sweep specialised to the exchange features its
 // tile actually touches. A wave away from every exchanged face (most of them:
 // not in the first/last x chunk, not in the first/last y row of tiles, not in a
@@ -681,17 +611,11 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
 #define IGG_HX_SWEEP_R(F)                                                                                \
   hx_sweep<T, BY, RY, VZ, PF, BZ, DF, (F)>(t2, t, cpp, xi0, xi1, yi0, yi1, zi0, zi1, xo0, xo1, yo0, yo1, \
                                            zo0, zo1, a, clo, chi)
-  if constexpr (FZ != 0) {
-    if (blockIdx.x < a.uz_blocks) {  // in-kernel z unpack (HxScal::uz_blocks)
-      hx_unpack_z(t, zi0, zi1, a);
-      return;
-    }
-  }
   if constexpr ((FX | FY | FZ) == 0 || (FEAT & 2048) != 0) {
     IGG_HX_SWEEP(FEAT);  // nothing to specialise, or specialisation disabled (FEAT 2048)
   } else {
     constexpr int W = 64 * VZ * BZ;
-    const HxTile<T> tile = hx_tile(a, blockIdx.x - a.uz_blocks, gridDim.x - a.uz_blocks);
+    const HxTile<T> tile = hx_tile(a, blockIdx.x, gridDim.x);
     const int64_t tz = tile.tz, ty = tile.ty, cx = tile.cx;
     const int64_t n0 = a.n0, n1 = a.n1, n2 = a.n2;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -719,11 +643,6 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     // neighbour reads or writes. (Counted on the host by hx_feature_waves.)
     const bool ks = a.sync.my_flags != nullptr && sel != 0;
     const uint64_t kc = ks ? step_sync_enter(a.sync, threadIdx.x & 63) : 0;
-    if constexpr (FZ != 0) {
-      // in-kernel z unpack: a wave holding a received z edge reads that halo
-      // from the field only after the unpack workgroups published it
-      if (a.uz_blocks > 0 && ((wz_lo && zi0) || (wz_hi && zi1))) hx_unpack_wait(a);
-    }
     // Peel (a.peel): an x-chunk wave needs the x exchange only at x = 1 (reads
     // plane 0 from the arena, sends plane 1) and x = n0-2 (sends it, reads
     // plane n0-1); the planes in between are swept with the x features
@@ -843,30 +762,7 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   const int64_t ch_all = std::max<int64_t>(1, (len0 * tiles + target - 1) / target);
   const int64_t nch = std::max<int64_t>(1, (len0 + ch_all - 1) / ch_all);
   a.ch = (len0 + nch - 1) / nch;
-  int64_t blocks = tiles * ((len0 + a.ch - 1) / a.ch);
-  // in-kernel z unpack: extra workgroups at the front of the grid (dispatched
-  // first) when this step has received z faces (HaloIOArgs::uz)
-  a.uz_blocks = 0;
-  a.uz_flags = nullptr;
-  a.uz_wait_arrival = 0;
-  a.uz_nrank = 0;
-  a.uz_timeout = io.uz_timeout;
-  if constexpr ((FEAT & (4 | 8)) != 0) {
-    if (io.uz && (io.in[2][0] || io.in[2][1])) {
-      if (!io.uz_flags) fail("diffusion3d (fused halo): in-kernel z unpack without a flag block");
-      static const int64_t ub = [] {
-        const char* e = std::getenv("IGG_UZ_BLOCKS");
-        return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t{64};
-      }();
-      a.uz_blocks = ub;
-      a.uz_flags = io.uz_flags;
-      a.uz_wait_arrival = io.uz_wait_arrival ? 1 : 0;
-      a.uz_nrank = io.uz_nrank;
-      a.uz_rank[0] = io.uz_rank[0];
-      a.uz_rank[1] = io.uz_rank[1];
-      blocks += ub;
-    }
-  }
+  const int64_t blocks = tiles * ((len0 + a.ch - 1) / a.ch);
   if (blocks > 0x7fffffffLL) fail("diffusion3d (fused halo): grid too large");
   a.rdx2 = static_cast<T>(d.rd2[0]);
   a.rdy2 = static_cast<T>(d.rd2[1]);
@@ -951,8 +847,7 @@ void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStre
     // Direct z (FEAT 203 = 207 without z-in): the z sends land in the
     // receivers' field halo elements, so the z-edge waves read their halo
     // from the field like every other wave and carry only the send code.
-    if ((io.in[2][0] || io.in[2][1]) && !io.uz)
-      fail("diffusion3d (fused halo): direct z mode with z arena input");
+    if (io.in[2][0] || io.in[2][1]) fail("diffusion3d (fused halo): direct z mode with z arena input");
     // halo_z contract (HaloIOArgs::zh): a side whose halo column a neighbour
     // writes during this kernel (direct z) never takes whole-line edge stores
     for (int sd = 0; sd < 2; ++sd)

@@ -33,8 +33,6 @@ struct PutFlags {
   static constexpr int EPOCH = 0;     // completed exchanges (the running one is EPOCH + 1)
   static constexpr int ERROR = 1;     // 0 ok, else 1 + code of the first timeout
   static constexpr int COUNT = 2;     // exchanging waves retired in the running step (in-kernel step sync)
-  static constexpr int UCOUNT = 3;    // in-kernel z unpack: workgroups done in the running step (fused_impl.hpp)
-  static constexpr int UEPOCH = 4;    // in-kernel z unpack: the last step whose z halo is unpacked
   static constexpr int ARRIVED = 8;   // [ARRIVED + r]: last epoch rank r's data arrived
   __host__ __device__ static inline int freed(int nranks) { return ARRIVED + nranks; }  // [freed + r]
   __host__ __device__ static inline int words(int nranks) { return ARRIVED + 2 * nranks; }

@@ -84,16 +84,6 @@ struct HaloIOArgs {
   int zh[2] = {-1, -1};
   // The z sends (out[2]) go into arena regions, not into a neighbour's field.
   bool z_out_arena = true;
-  // In-kernel z unpack (FusedHalo send mode bit 128): in[2] are this step's
-  // received z regions, copied into t's z halo columns by extra workgroups of
-  // the same launch; the sweep reads the z halo from the field (no z receive
-  // code) after those workgroups published (put.hpp UEPOCH in uz_flags).
-  bool uz = false;
-  uint64_t* uz_flags = nullptr;
-  int uz_rank[2] = {0, 0};
-  int uz_nrank = 0;
-  bool uz_wait_arrival = false;
-  int64_t uz_timeout = 0;
   // In-kernel step synchronisation (put.hpp StepSync; FusedHalo): the launch
   // takes it when it can count its exchanging waves and then sets *sync_used
   // (otherwise the caller follows the kernel with the sync kernel).

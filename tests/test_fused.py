@@ -326,28 +326,6 @@ def test_fused_z_unpack_matches_update_halo(gpu, variant, mode, periods):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [128, 136, 137, 144, 152])  # in-kernel z unpack (+8 peel, +1 deferred, +16 step sync)
-@pytest.mark.parametrize("variant", [0, 9, 40, 42, 44])
-@pytest.mark.parametrize("periods", [(1, 1, 1), (1, 0, 1), (0, 0, 1)])
-def test_fused_z_unpack_in_kernel_matches_update_halo(gpu, variant, mode, periods):
-    """Send mode bit 128: the received z faces are copied into the field's z
-    halo columns by extra workgroups at the front of the next step's launch,
-    which the z-edge waves wait for; eager steps and graph replays, bitwise
-    the same as stencil + update_halo_."""
-    a, b = _pair((34, 29, 136), periods, torch.float64, variant, mode=mode)
-    a.run(3)
-    b.run(3)
-    b.capture(steps=4)
-    a.run(9)
-    b.run(9)
-    b.sync_halo()
-    torch.cuda.synchronize()
-    b.check()
-    assert torch.equal(a.T, b.T)
-    igg.finalize_global_grid(finalize_MPI=False)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("mode", [80, 88])  # z unpack + in-kernel step sync (+ 8 peel)
 @pytest.mark.parametrize("variant", [0, 9, 40, 42])
 @pytest.mark.parametrize("periods", [(1, 1, 1), (0, 0, 1)])
@@ -370,7 +348,7 @@ def test_fused_z_unpack_in_kernel_sync_matches_update_halo(gpu, variant, mode, p
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,mode", [(44, 72), (14, 64), (42, 73), (0, 136), (14, 152)])
+@pytest.mark.parametrize("variant,mode", [(44, 72), (14, 64), (42, 73)])
 def test_fused_z_unpack_f32_graph_loopback(gpu, variant, mode):
     """z unpack in f32, under hipGraph replays with odd step counts and through
     the loopback emulation's remote path."""

@@ -236,10 +236,7 @@ def test_gather_pull_failure_is_collective_gpu(inject, expect):
                                                # z unpack (mode bit 64) on 2x2x2 corner ranks and periodic
                                                (8, (18, 20, 136, 5, 0, 0), ("9", "72")),
                                                (8, (16, 18, 24, 6, 1, 1), ("42", "73")),
-                                               (2, (24, 20, 64, 6, 0, 1), ("0", "64")),
-                                               # in-kernel z unpack (mode bit 128)
-                                               (8, (18, 20, 136, 5, 0, 0), ("40", "136")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("9", "128"))])
+                                               (2, (24, 20, 64, 6, 0, 1), ("0", "64"))])
 def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
     # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
@@ -254,8 +251,7 @@ def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
                                                (8, (18, 20, 40, 7, 1, 0), ("0", "5")),
                                                # z unpack: the unpack kernel waits for the z senders itself
                                                (8, (18, 20, 136, 5, 0, 0), ("0", "72")),
-                                               (2, (24, 20, 64, 6, 0, 1), ("0", "64")),
-                                               (8, (18, 20, 136, 5, 0, 0), ("0", "136"))])
+                                               (2, (24, 20, 64, 6, 0, 1), ("0", "64"))])
 def test_diffusion_gpu_multirank_fused_in_kernel_sync(nprocs, cfg, kernel):
     """The step synchronisation inside the fused kernel across processes
     (forced: ranks sharing one GPU default to the sync kernel, because waiting
