@@ -320,6 +320,30 @@ def _median(xs):
     return s[len(s) // 2] if len(s) % 2 else 0.5 * (s[len(s) // 2 - 1] + s[len(s) // 2])
 
 
+def _begin_local_steps(model) -> dict | None:
+    """State kept across the efficiency phase's local steps, for models whose
+    halo exchange cannot repair what local steps leave (no ``exchange_halos``:
+    the acoustic model's staggered fields have planes computed on both ranks
+    that drift apart, models/acoustic2d.py local_step; a fused post-check
+    after this phase failed without the restore, profiles/r5_checks/c15)."""
+    if hasattr(model, "exchange_halos"):
+        return None
+    return {n: getattr(model, n).clone() for n in _state(model)}
+
+
+def _end_local_steps(model, saved: dict | None) -> None:
+    """After the local steps: restore the kept state by content (buffer roles
+    may have swapped) or re-exchange the halos; then the next fused step
+    starts with its entry barrier (mark_modified)."""
+    if saved is None:
+        model.exchange_halos()  # also marks the fields modified
+        return
+    for n, t in saved.items():
+        getattr(model, n).copy_(t)
+    if hasattr(model, "mark_modified"):
+        model.mark_modified()
+
+
 def measure_efficiency(model, comm, log, graph: bool, k: int, pairs: int = EFF_PAIRS) -> dict | None:
     """Weak-scaling efficiency measured in THIS job: E = t_it(local) / t_it(step).
 
@@ -333,11 +357,12 @@ def measure_efficiency(model, comm, log, graph: bool, k: int, pairs: int = EFF_P
     brackets (MAX over ranks each). ``pairs`` interleaved [local, step] pairs
     of ``k`` steps, medians. This removes the box-to-box spread (+-2-3 %)
     that a ratio of two different jobs' numbers carries (E(N) =
-    t_it(1) / t_it(N)). Collective. The halo planes are left unexchanged by
-    the local steps: the caller takes any starting-state snapshot afterwards
-    (the model is told with ``mark_modified``)."""
+    t_it(1) / t_it(N)). Collective. The local steps leave the halo planes
+    unexchanged; ``_end_local_steps`` repairs the state at the end. The
+    caller takes any starting-state snapshot afterwards."""
     if not hasattr(model, "local_step"):
         return None
+    saved = _begin_local_steps(model)
     k = max(2, k + (k % 2))  # even: the ping-pong buffers keep their roles
     on_gpu = getattr(model, "device", None) is not None and model.device.type == "cuda"
     gl = None
@@ -376,8 +401,7 @@ def measure_efficiency(model, comm, log, graph: bool, k: int, pairs: int = EFF_P
         tm.append(a)
         own_m.append(b)
     used_graph, gl = gl is not None, None
-    if hasattr(model, "mark_modified"):
-        model.mark_modified()  # the local steps wrote the fields outside the exchange protocol
+    _end_local_steps(model, saved)
     t_loc, t_step = _median(tl), _median(tm)
     per_rank_loc = _all_ranks(comm, _median(own_l))
     per_rank_step = _all_ranks(comm, _median(own_m))
@@ -1283,8 +1307,8 @@ def main():
             log(f"hipGraph capture failed, running eager: {graph_error}")
     # Same-process weak-scaling efficiency (config.efficiency): interleaved
     # pairs of the 1-GPU run's local problem and the real step, on these GPUs
-    # and processes. Before the snapshot and the warm load below: it leaves the
-    # halo planes unexchanged, which no later check depends on.
+    # and processes. Before the snapshot and the warm load below (it ends with
+    # one halo exchange: the local steps leave the halos unexchanged).
     eff = None
     if os.environ.get("IGG_BENCH_EFFICIENCY", "1") != "0":
         PH.enter("efficiency", _path_key(model), deadline=300)

@@ -199,7 +199,12 @@ class Acoustic2D:
         """One step of the LOCAL problem (what a rank without neighbours runs:
         the staggered update, no exchange - update_halo_ with PROC_NULL
         neighbours is a no-op, reference src/update_halo.jl:40-42). Timing
-        only (the bench's same-process efficiency); halos stay unexchanged."""
+        only (the bench's same-process efficiency, which restores the state
+        afterwards). No halo exchange repairs the state it leaves: the
+        staggered fields' overlap is 3 along their staggered dim, so one plane
+        next to each halo is computed on both ranks (never exchanged) and
+        drifts apart under local steps, and the fused step is bitwise equal to
+        the update_halo_ path only from states where those copies agree."""
         self._update(self.P2, self.Vx2, self.Vy2, self.P, self.Vx, self.Vy)
         self.P, self.P2 = self.P2, self.P
         self.Vx, self.Vx2 = self.Vx2, self.Vx

@@ -256,6 +256,13 @@ class Diffusion3D:
         self._fprimed = False
         self._fentry = True
 
+    def exchange_halos(self) -> None:
+        """Make T's halo planes equal the neighbours' (update_halo_(T);
+        collective) and mark the fields modified: after ``local_step`` calls
+        the state is again one the time loop could have produced."""
+        update_halo_(self.T)
+        self.mark_modified()
+
     def close(self) -> None:
         """Release the fused exchange's peer mesh (collective: every rank)."""
         if self._fh is not None:
@@ -435,7 +442,7 @@ class Diffusion3D:
         (reference: src/update_halo.jl:40-42, no neighbour -> nothing sent).
         Used by the bench's same-process efficiency E = t(local) / t(step).
         Leaves the halo planes unexchanged: timing only (callers that go on
-        with real steps call ``mark_modified`` afterwards)."""
+        with real steps call ``exchange_halos`` afterwards)."""
         T, T2 = self.T, self.T2
         stencil.diffusion3d_(T2, T, self.Cp, boxes=self.inner, halo_z=self.halo_z, **self._kw())
         self.T, self.T2 = T2, T

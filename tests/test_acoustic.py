@@ -207,6 +207,46 @@ def test_gpu_fused_loopback_graph_and_switch(gpu):
     igg.finalize_global_grid(finalize_MPI=False)
 
 
+def _bench_module():
+    import importlib.util as ilu
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+    spec = ilu.spec_from_file_location("bench_mod", path)
+    b = ilu.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("loopback", [False, True])
+def test_gpu_fused_after_local_steps(gpu, loopback):
+    """The bench's efficiency phase runs local steps (no exchange) on the
+    model, then restores its state: the fused step is bitwise equal to the
+    update_halo_ path afterwards (a halo exchange alone does not repair the
+    staggered fields' doubly computed planes: the fused post-check failed
+    after it, profiles/r5_checks/c16)."""
+    bench = _bench_module()
+    a, b = _fused_pair((66, 64), (1, 1), torch.float32, loopback=loopback)
+    for m in (a, b):
+        m.run(3)
+    saved = bench._begin_local_steps(b)
+    assert saved is not None
+    for _ in range(5):
+        b.local_step()
+    bench._end_local_steps(b, saved)
+    assert b._entry
+    b.capture(steps=4)
+    a.run(1)  # capture ran one eager step
+    a.run(12)
+    b.run(12)
+    torch.cuda.synchronize()
+    b.check()
+    assert _same(a, b)
+    b.close()
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("nprocs,per,sync_kernel", [(2, 1, 0), (4, 0, 0), (4, 1, 0), (4, 1, 1)])
 def test_gpu_fused_multirank(nprocs, per, sync_kernel):

@@ -210,3 +210,55 @@ def test_ab_budget_orders_and_truncates():
     _t.sleep(0.01)
     assert not bud.left()
     assert b._ABBudget(_C(), seconds=100.0).left()
+
+
+@pytest.mark.parametrize("model", ["acoustic", "diffusion"])
+def test_efficiency_phase_leaves_a_consistent_state(model):
+    """The efficiency phase's local steps (no exchange) are undone for the
+    timed region: the acoustic model's state is restored bitwise (its
+    staggered fields have planes computed on two ranks that drift apart), the
+    diffusion model's halos are re-exchanged (periodic: halo = wrapped
+    interior)."""
+    import importlib.util as ilu
+
+    import torch
+
+    import igg
+
+    spec = ilu.spec_from_file_location("bench_mod", BENCH)
+    b = ilu.module_from_spec(spec)
+    spec.loader.exec_module(b)
+
+    class _C:
+        size = 1
+
+        def barrier(self):
+            pass
+
+    b._BRACKET["gpu"] = False
+    if model == "acoustic":
+        from igg.models.acoustic2d import Acoustic2D
+
+        igg.init_global_grid(20, 16, 1, periodx=1, periody=1, quiet=True, init_MPI=False)
+        m = Acoustic2D(dtype=torch.float64)
+    else:
+        from igg.models.diffusion3d import Diffusion3D
+
+        igg.init_global_grid(12, 10, 8, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+        m = Diffusion3D(dtype=torch.float64)
+    try:
+        m.run(3)
+        before = {n: getattr(m, n).clone() for n in b._state(m)}
+        e = b.measure_efficiency(m, _C(), lambda s: None, False, 4)
+        assert e is not None and e["steps"] == 4
+        if model == "acoustic":
+            assert all(torch.equal(before[n], getattr(m, n)) for n in before)
+            assert m._entry
+        else:
+            T = m.T
+            assert not torch.equal(before["T"], T)  # the phase's real steps advanced it
+            for d in range(3):
+                lo, hi = T.select(d, 0), T.select(d, T.shape[d] - 1)
+                assert torch.equal(lo, T.select(d, T.shape[d] - 2)) and torch.equal(hi, T.select(d, 1))
+    finally:
+        igg.finalize_global_grid(finalize_MPI=False)
