@@ -189,7 +189,7 @@ def test_gather_async_gpu(nprocs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nprocs", [2, 4])
+@pytest.mark.parametrize("nprocs", [pytest.param(2, marks=pytest.mark.slow), 4])
 def test_gather_pull_staged_chunks_gpu(nprocs):
     """Blocks too large to export whole (above 2 GiB on the real runtime,
     above 100 / 400 bytes here) are staged in chunks of whole x-planes and
@@ -215,19 +215,22 @@ def test_gather_pull_failure_is_collective_gpu(inject, expect):
 
 
 # --- fused halo exchange (stencil kernel stores into the neighbours' arenas)
+SLOW = pytest.mark.slow  # redundant cases: IGG_TEST_SLOW=1 (conftest.py)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("nprocs,cfg,kernel", [(2, (24, 20, 64, 6, 0, 0), ("0", "0")),
                                                (4, (20, 22, 32, 5, 1, 1), ("9", "1")),
-                                               (8, (18, 20, 40, 7, 0, 0), ("0", "1")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("50", "0")),
+                                               pytest.param(8, (18, 20, 40, 7, 0, 0), ("0", "1"), marks=SLOW),
+                                               pytest.param(8, (16, 18, 24, 6, 1, 1), ("50", "0"), marks=SLOW),
                                                # per-side wave classes of variant 40 and the edge-lane z
                                                # form of 42 (n2 > 64*VZ+VZ) on one-sided (non-periodic) ranks
                                                (4, (20, 22, 136, 5, 0, 0), ("40", "0")),
                                                (8, (18, 20, 136, 5, 0, 1), ("42", "0")),
                                                # direct z (mode bit 4): z faces into the neighbours' T2
-                                               (2, (24, 20, 64, 6, 1, 0), ("40", "4")),
+                                               pytest.param(2, (24, 20, 64, 6, 1, 0), ("40", "4"), marks=SLOW),
                                                (8, (18, 20, 136, 5, 0, 1), ("42", "4")),
-                                               (8, (16, 18, 24, 6, 1, 1), ("0", "5")),
+                                               pytest.param(8, (16, 18, 24, 6, 1, 1), ("0", "5"), marks=SLOW),
                                                # peeled x planes (mode bit 8) with remote x neighbours
                                                (2, (40, 66, 136, 6, 1, 0), ("42", "12")),
                                                (8, (34, 66, 136, 5, 1, 1), ("40", "8")),
@@ -265,7 +268,8 @@ def test_diffusion_gpu_multirank_fused_in_kernel_sync(nprocs, cfg, kernel):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nprocs,kernel", [(4, ("0", "0")), (8, ("0", "1")), (8, ("40", "4"))])
+@pytest.mark.parametrize("nprocs,kernel", [pytest.param(4, ("0", "0"), marks=pytest.mark.slow), (8, ("0", "1")),
+                                            pytest.param(8, ("40", "4"), marks=pytest.mark.slow)])
 def test_fused_soak_with_rank_skew(nprocs, kernel):
     """Thousands of graph-replayed fused steps with random host skew between
     ranks stay bitwise equal to stencil + update_halo_."""
