@@ -24,6 +24,7 @@ from .parallel.grid import (  # noqa: F401
 )
 from .parallel.device import select_device  # noqa: F401
 from .parallel.halo import update_halo, update_halo_  # noqa: F401
+from .parallel.transport_select import select_transport  # noqa: F401
 from .parallel.gather import gather, gather_, gather_async_  # noqa: F401
 from .utils.tools import coords_g, nx_g, ny_g, nz_g, tic, toc, x_g, y_g, z_g  # noqa: F401
 from .utils.checkpoint import load_checkpoint, save_checkpoint  # noqa: F401
@@ -33,5 +34,5 @@ __version__ = "0.1.0"
 __all__ = [
     "init_global_grid", "finalize_global_grid", "update_halo_", "update_halo", "gather_", "gather",
     "select_device", "nx_g", "ny_g", "nz_g", "x_g", "y_g", "z_g", "tic", "toc", "get_global_grid",
-    "IGGError", "coords_g", "gather_async_", "save_checkpoint", "load_checkpoint",
+    "IGGError", "coords_g", "gather_async_", "save_checkpoint", "load_checkpoint", "select_transport",
 ]

@@ -388,6 +388,38 @@ def scenario_put_after_model(n, graph, steps):
     print(f"rank {me} put after model OK", flush=True)
 
 
+def scenario_select_transport(dev):
+    """select_transport: on GPU ranks sharing one device, 'put' passes the
+    probe check against the host-staged exchange, RCCL is skipped (it refuses
+    duplicate devices) and update_halo_ runs on 'put' afterwards, bitwise vs
+    the expected halos; on a CPU grid nothing is switched."""
+    device = _device(dev)
+    n = 20
+    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n - 2, 12, quiet=True, select_device=False,
+                                                          device_type="none" if dev == "cpu" else "AMDGPU")
+    gg = igg.get_global_grid()
+    A = torch.zeros(n, n - 2, 12, dtype=torch.float64)
+    encode(A)
+    ref = expected_after_halo(A, has_halo(A, gg), gg.neighbors.tolist())
+    X = zero_boundaries(A.clone()).to(device)
+    before = X.clone()
+    res = igg.select_transport(X, steps=3)
+    print(f"rank {me} select_transport {res}", flush=True)
+    assert torch.equal(X, before), "select_transport modified its argument"
+    if dev == "cpu":
+        assert "reason" in res and not res["checked"]
+    else:
+        assert res["checked"]["put"] == "ok", res
+        assert res["checked"]["rccl"].startswith("skipped"), res
+        assert res["chosen"] == "put" and res["ms"]["put"] > 0, res
+    igg.update_halo_(X)
+    got = X.cpu()
+    bad = (got != ref).nonzero()
+    assert bad.shape[0] == 0, f"rank {me}: halo mismatch after select_transport at {bad[:6].tolist()}"
+    igg.finalize_global_grid()
+    print(f"rank {me} select transport OK", flush=True)
+
+
 def scenario_put_regrow():
     """Put transport with field sets that force the receive arenas to grow
     (a collective re-export of IPC memory) several times (growth floor

@@ -214,6 +214,14 @@ def test_gather_pull_failure_is_collective_gpu(inject, expect):
     run_ranks(3, "gather_fail", expect, env_extra=dict(PUT_ENV, IGG_INJECT_FAIL=inject), timeout=120)
 
 
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_select_transport(dev):
+    """igg.select_transport: every candidate checked bitwise against the
+    host-staged exchange, the fastest checked one kept (GPU ranks sharing a
+    device: 'put'; RCCL skipped); a CPU grid has nothing to choose."""
+    run_ranks(2, "select_transport", dev, timeout=150)
+
+
 # --- fused halo exchange (stencil kernel stores into the neighbours' arenas)
 SLOW = pytest.mark.slow  # redundant cases: IGG_TEST_SLOW=1 (conftest.py)
 

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 SECTIONS = [
     ("Grid", "igg", ["init_global_grid", "finalize_global_grid", "get_global_grid", "select_device"]),
-    ("Halo update", "igg", ["update_halo_"]),
+    ("Halo update", "igg", ["update_halo_", "select_transport"]),
     ("Gather", "igg", ["gather_", "gather_async_"]),
     ("Global sizes and coordinates, timing", "igg",
      ["nx_g", "ny_g", "nz_g", "x_g", "y_g", "z_g", "coords_g", "tic", "toc"]),
