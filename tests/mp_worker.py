@@ -392,7 +392,8 @@ def scenario_select_transport(dev):
     """select_transport: on GPU ranks sharing one device, 'put' passes the
     probe check against the host-staged exchange, RCCL is skipped (it refuses
     duplicate devices) and update_halo_ runs on 'put' afterwards, bitwise vs
-    the expected halos; on a CPU grid nothing is switched."""
+    the expected halos; one rank per device (mgpu): both pass and the faster
+    is kept; on a CPU grid nothing is switched."""
     device = _device(dev)
     n = 20
     me, dims, nprocs, coords, comm = igg.init_global_grid(n, n - 2, 12, quiet=True, select_device=False,
@@ -408,10 +409,13 @@ def scenario_select_transport(dev):
     assert torch.equal(X, before), "select_transport modified its argument"
     if dev == "cpu":
         assert "reason" in res and not res["checked"]
-    else:
+    elif dev == "gpu":  # every rank on device 0
         assert res["checked"]["put"] == "ok", res
         assert res["checked"]["rccl"].startswith("skipped"), res
         assert res["chosen"] == "put" and res["ms"]["put"] > 0, res
+    else:  # mgpu: one rank per device, both checked, the faster kept
+        assert res["checked"] == {"put": "ok", "rccl": "ok"}, res
+        assert res["chosen"] == min(res["ms"], key=res["ms"].get), res
     igg.update_halo_(X)
     got = X.cpu()
     bad = (got != ref).nonzero()

@@ -17,7 +17,7 @@ budget, not launches x 170 s; with the single-GPU tests (<= 300 s) that
 stays inside the driver's 900 s step cap. The launches run in the order of
 their value, so a spent budget drops the least essential ones:
 
-    1  8-rank halo oracle (RCCL sequential / one-phase / auto, put) + ring
+    1  8-rank halo oracle (RCCL sequential / one-phase / auto, put) + ring + select_transport
     2  2-rank suite (left == right periodic neighbour: same-peer ordering)
     3  4-rank suite (2x2x1)
     4  8-rank gather (pull and RCCL paths, roots 0 and 7) + gather_async + collectives
@@ -104,6 +104,7 @@ def test_halo_and_ring_8_ranks():
             items.append(halo(cfg, f"{RCCL};IGG_HALO_MODE={mode}"))
     items.append(halo((7, 5, 6, 1, 1, 1), PUT))
     items.append(f"ring:mgpu|{RCCL}")
+    items.append(f"select_transport:mgpu|{MGPU}")
     suite(8, *items)
 
 
