@@ -62,7 +62,7 @@ import time
 # without z neighbours, z-edge waves 6-10 % faster than 40's with them. Its
 # deferred-send mode is kept in the A/B for real xGMI links, where a remote
 # store's acknowledgement is slower than in the loopback measurements.
-FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 3), (14, 0, 3),
+FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 2), (9, 0, 3), (14, 0, 3),
                     (40, 0, 2), (42, 0, 2), (42, 1, 2), (50, 0, 2), (50, 1, 2), (50, 1, 3))
 # Direct z (send mode bit 4: the z faces go straight into the neighbours' next
 # T, no z receive code in the z-edge waves; igg/fused.hpp). Only with a z
@@ -85,13 +85,15 @@ FUSED_ZUNPACK_F32 = ((44, 64, 4), (14, 64, 3))
 # rehearsal, profiles/r4_shapes/ per rank shape; the in-kernel-sync forms, bit
 # 16, are derived from the front later): tried first, so a spent A/B budget
 # (IGG_BENCH_AB_BUDGET) drops forms that never won anywhere.
+#   (9, 8, 2) / (9, 0, 2): the 2x2x2 corner's best forms on every round-5 box
+#   (0.2-1.1 % ahead of their 3-round forms: profiles/r5_unpack/, r5_shapes/)
 #   (9, 8, 3)  8-rank 2x2x2 rehearsal winner (r4), (9, 0, 3) 2x2x2 corner (r4 pass 4)
 #   (42, 12, 2) interior + corner f64 (m28 = 12|16), (42, 9, 2) x+/xy+ (m25 = 9|16)
 #   (14, 8, 3) f32 x/xy (m24 = 8|16), (44, 44, 4) / (44, 12, 4) f32 corner
 #   (9, 72, 3) / (42, 72, 2): the round-5 z-unpack corner forms (no record yet;
 #   right behind the record's front so a spent budget still times them)
-FUSED_WIN_ORDER = ((9, 8, 3), (42, 12, 2), (42, 9, 2), (9, 0, 3), (9, 72, 3), (42, 72, 2), (42, 8, 2),
-                   (14, 8, 3), (44, 44, 4), (44, 12, 4), (44, 72, 4), (42, 4, 2), (0, 12, 3), (42, 0, 2),
+FUSED_WIN_ORDER = ((9, 8, 2), (9, 0, 2), (9, 8, 3), (42, 12, 2), (42, 9, 2), (9, 0, 3), (9, 72, 3), (42, 72, 2),
+                   (42, 8, 2), (14, 8, 3), (44, 44, 4), (44, 12, 4), (44, 72, 4), (42, 4, 2), (0, 12, 3), (42, 0, 2),
                    (40, 12, 2))
 
 
