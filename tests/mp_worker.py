@@ -249,6 +249,7 @@ def scenario_diffusion_fused(nx, ny, nz, steps, periodic, graph):
     a = Diffusion3D(dtype=torch.float64, device=device, variant=_plain(v))
     b = Diffusion3D(dtype=torch.float64, device=device, variant=_plain(v))
     b.fused_variant, b.fused_mode = v, int(os.environ.get("IGG_TEST_FUSED_MODE", "0"))
+    b.fused_rounds = int(os.environ.get("IGG_TEST_FUSED_ROUNDS", str(b.fused_rounds)))
     want = b.fused_mode
     assert b.set_fused(True), "fused mode unavailable"
     assert b.fused_variant == v, f"fused variant {v} is not compiled in this build"

@@ -63,11 +63,12 @@ RCCL = f"{MGPU};IGG_TRANSPORT=rccl"
 PUT = f"{MGPU};IGG_TRANSPORT=put;IGG_PUT_TIMEOUT=20"
 
 
-def fused(v, mode, *cfg):
+def fused(v, mode, *cfg, rounds=None):
     """Fused exchange (stencil stores its send planes over xGMI) vs stencil +
     update_halo_ (RCCL), bitwise on every rank."""
+    r = f";IGG_TEST_FUSED_ROUNDS={rounds}" if rounds else ""
     return f"diffusion_fused:{':'.join(map(str, cfg))}|{RCCL};IGG_PUT_TIMEOUT=20;IGG_TEST_VARIANT={v};" \
-           f"IGG_TEST_FUSED_MODE={mode}"
+           f"IGG_TEST_FUSED_MODE={mode}{r}"
 
 
 def soak(v, mode, rounds=40, per=40):
@@ -153,6 +154,8 @@ def test_fused_forms_and_diffusion_8_ranks():
           fused(40, 8, 34, 66, 136, 5, 1, 1),
           fused(44, 4, 18, 20, 136, 4, 1, 0),
           fused(9, 72, 18, 20, 136, 5, 0, 1),
+          fused(9, 0, 18, 20, 136, 5, 0, 0, rounds=2),
+          fused(9, 8, 34, 66, 136, 5, 0, 0, rounds=2),
           fused(42, 64, 16, 18, 136, 5, 1, 1),
           f"diffusion:mgpu:24:20:18:7:0|{RCCL}",
           f"diffusion:mgpu:24:20:18:7:0|{PUT}")

@@ -244,6 +244,9 @@ SLOW = pytest.mark.slow  # redundant cases: IGG_TEST_SLOW=1 (conftest.py)
                                                (8, (34, 66, 136, 5, 1, 1), ("40", "8")),
                                                # z-edge tiles first (mode bit 32) on one-sided corner ranks
                                                (8, (34, 66, 136, 5, 0, 0), ("42", "44")),
+                                               # tiling 9 with 2 grid rounds on 2x2x2 corner ranks (the
+                                               # corner's best form, the bench's first candidate)
+                                               (8, (18, 20, 136, 5, 0, 0), ("9", "8", "2")),
                                                # z unpack (mode bit 64) on 2x2x2 corner ranks and periodic
                                                (8, (18, 20, 136, 5, 0, 0), ("9", "72")),
                                                (8, (16, 18, 24, 6, 1, 1), ("42", "73")),
@@ -251,6 +254,8 @@ SLOW = pytest.mark.slow  # redundant cases: IGG_TEST_SLOW=1 (conftest.py)
 def test_diffusion_gpu_multirank_fused(nprocs, cfg, kernel):
     # ranks share one GPU on the test box: RCCL cannot, so sync_halo uses 'put'
     env = {**PUT_ENV, "IGG_PUT_TIMEOUT": "20", "IGG_TEST_VARIANT": kernel[0], "IGG_TEST_FUSED_MODE": kernel[1]}
+    if len(kernel) > 2:
+        env["IGG_TEST_FUSED_ROUNDS"] = kernel[2]
     if nprocs > 2:
         env["GPU_MAX_HW_QUEUES"] = "1"  # ranks share one GPU: no queue oversubscription (profiles/r2_reh8/)
     run_ranks(nprocs, "diffusion_fused", *cfg, env_extra=env, timeout=170)
