@@ -79,4 +79,42 @@ __device__ inline void step_sync_exit(const StepSync& s, int lane, uint64_t c) {
   }
 }
 
+// Per-workgroup forms for kernels whose workgroups hold several exchanging
+// waves (diffusion3d_hx_kernel). `wsync` is the workgroup's LDS block
+// {entered, go, c, retired}, zeroed behind a barrier before any wave uses it.
+// Enter: the workgroup's first exchanging wave runs step_sync_enter (the
+// flag polls and the system acquire, which also drops stale lines from the
+// CU's L1 that every wave of the workgroup shares) and publishes c in LDS;
+// the others wait for it there. The poller is a wave of the same (resident)
+// workgroup and sets `go` even after a timed-out wait, so the waiters always
+// finish.
+__device__ inline uint64_t step_sync_enter_wg(const StepSync& s, int lane, uint64_t* wsync) {
+  uint64_t first = 0;
+  if (lane == 0)
+    first = __hip_atomic_fetch_add(wsync + 0, uint64_t{1}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  first = __shfl(first, 0);
+  if (first == 0) {
+    const uint64_t c = step_sync_enter(s, lane);
+    if (lane == 0) {
+      wsync[2] = c;
+      __hip_atomic_store(wsync + 1, uint64_t{1}, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return c;
+  }
+  while (__hip_atomic_load(wsync + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+  return wsync[2];
+}
+
+// Exit: every exchanging wave waits for its own stores (s_waitcnt 0) and
+// counts itself in LDS; the workgroup's last one counts the workgroup in
+// COUNT (step_sync_exit; StepSync::feat_waves = exchanging workgroups), and
+// the launch's last workgroup publishes step c + 1.
+__device__ inline void step_sync_exit_wg(const StepSync& s, int lane, uint64_t c, uint64_t* wsync, int n_ex) {
+  __builtin_amdgcn_s_waitcnt(0);
+  uint64_t old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(wsync + 3, uint64_t{1}, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = __shfl(old, 0);
+  if (old + 1 == static_cast<uint64_t>(n_ex)) step_sync_exit(s, lane, c);
+}
+
 }  // namespace igg

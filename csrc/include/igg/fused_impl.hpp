@@ -640,9 +640,32 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
     const int64_t t_start = a.stamps ? wall_clock64() : 0;
     // The exchanging waves (sel != 0) synchronise the step with the
     // neighbours (StepSync, put.hpp); the others never touch memory a
-    // neighbour reads or writes. (Counted on the host by hx_feature_waves.)
+    // neighbour reads or writes. Per workgroup: its first exchanging wave
+    // polls the flags (one system acquire for the CU's L1) and hands the step
+    // number to the others through LDS; its last one counts the workgroup
+    // (hx_feature_wgs on the host) - a 2x2x2 corner has ~1,100 exchanging
+    // waves, whose per-wave uncached polls and counts slowed every wave.
     const bool ks = a.sync.my_flags != nullptr && sel != 0;
-    const uint64_t kc = ks ? step_sync_enter(a.sync, threadIdx.x & 63) : 0;
+    __shared__ uint64_t wsync[4];  // entered, go, step number c, retired
+    if (a.sync.my_flags != nullptr) {  // launch-uniform: every wave of the workgroup
+      if (threadIdx.x < 4) wsync[threadIdx.x] = 0;
+      __syncthreads();
+    }
+    int n_ex = 0;  // exchanging waves of this workgroup (same rule as sel, every wave computes it)
+    if (ks) {
+      int qy = 0, qz = 0;
+      for (int j = 0; j < BY; ++j) {
+        const int64_t yj = 1 + ty * (BY * RY) + j * RY, nvj = min<int64_t>(RY, n1 - 1 - yj);
+        qy += (FY != 0 && ((yj <= 1 && (yi0 || yo0)) || (yj + nvj >= n1 - 1 && (yi1 || yo1)))) ? 0 : 1;
+      }
+      for (int k = 0; k < BZ; ++k) {
+        const int64_t zk = tz * W + k * (64 * VZ);
+        const bool lo = zk == 0 && (zi0 || zo0), hi = zk <= n2 - VZ && n2 - VZ < zk + 64 * VZ && (zi1 || zo1);
+        qz += (FZ != 0 && (lo || hi)) ? 0 : 1;
+      }
+      n_ex = __builtin_amdgcn_readfirstlane(wx ? BY * BZ : BY * BZ - qy * qz);
+    }
+    const uint64_t kc = ks ? step_sync_enter_wg(a.sync, threadIdx.x & 63, wsync) : 0;
     // Peel (a.peel): an x-chunk wave needs the x exchange only at x = 1 (reads
     // plane 0 from the arena, sends plane 1) and x = n0-2 (sends it, reads
     // plane n0-1); the planes in between are swept with the x features
@@ -674,7 +697,7 @@ diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __re
         default: IGG_HX_SWEEP_ZS(FEAT); break;
       }
     }
-    if (ks) step_sync_exit(a.sync, threadIdx.x & 63, kc);
+    if (ks) step_sync_exit_wg(a.sync, threadIdx.x & 63, kc, wsync, n_ex);
     if (a.stamps) {
       // one vector store per wave (lane 0; lane-dependent address -> VGPR store)
       const int lane = threadIdx.x & 63;
@@ -705,33 +728,42 @@ int resident(const void* kernel, int block, size_t lds = 0) {
   return r;
 }
 
-// The number of waves of a launch that run an exchange form (sel != 0 in
-// diffusion3d_hx_kernel): the same per-wave rule on the host. The rule is
-// separable - the x part depends on the chunk, the y part on the wave's rows,
-// the z part on its z tile - so the waves with no feature are a product.
+// Workgroups of the launch with at least one exchanging wave (sel != 0 in
+// diffusion3d_hx_kernel, the same per-wave rule on the host): the units the
+// in-kernel step sync counts (step_sync_exit_wg). The rule is separable - the
+// x part depends on the chunk, the y part on the wave's rows, the z part on
+// its z tile - and the waves of a workgroup share its chunk, so a workgroup
+// has none if its chunk, all its wave rows and all its z columns are
+// feature-free: a product.
 template <int BY, int RY, int VZ, int BZ, int FEAT>
-int64_t hx_feature_waves(int64_t n0, int64_t n1, int64_t n2, int64_t ch, int64_t nty, int64_t ntz,
-                         const HaloIOArgs& io) {
+int64_t hx_feature_wgs(int64_t n0, int64_t n1, int64_t n2, int64_t ch, int64_t nty, int64_t ntz,
+                       const HaloIOArgs& io) {
   constexpr int FX = FEAT & (1 | 64), FY = FEAT & (2 | 128), FZ = FEAT & (4 | 8);
   constexpr int W = 64 * VZ * BZ;
   auto on = [&](int d, int s) { return io.in[d][s] != 0 || io.out[d][s] != 0; };
   const int64_t nch = (n0 - 2 + ch - 1) / ch;
-  int64_t qx = 0, qy = 0, qz = 0;  // counts WITHOUT the feature
+  int64_t qx = 0, qy = 0, qz = 0;  // chunks / y tiles / z tiles WITHOUT the feature in any wave
   for (int64_t cx = 0; cx < nch; ++cx) {
     const int64_t xs = 1 + cx * ch, xe = std::min(xs + ch, n0 - 1);
     qx += !(FX != 0 && ((xs <= 1 && on(0, 0)) || (xe >= n0 - 2 && on(0, 1))));
   }
-  for (int64_t ty = 0; ty < nty; ++ty)
+  for (int64_t ty = 0; ty < nty; ++ty) {
+    bool none = true;
     for (int wy = 0; wy < BY; ++wy) {
       const int64_t y0 = 1 + ty * (BY * RY) + wy * RY, nv = std::min<int64_t>(RY, n1 - 1 - y0);
-      qy += !(FY != 0 && ((y0 <= 1 && on(1, 0)) || (y0 + nv >= n1 - 1 && on(1, 1))));
+      if (FY != 0 && ((y0 <= 1 && on(1, 0)) || (y0 + nv >= n1 - 1 && on(1, 1)))) none = false;
     }
-  for (int64_t tz = 0; tz < ntz; ++tz)
+    qy += none;
+  }
+  for (int64_t tz = 0; tz < ntz; ++tz) {
+    bool none = true;
     for (int wz = 0; wz < BZ; ++wz) {
       const int64_t zt = tz * W + wz * (64 * VZ);
-      qz += !(FZ != 0 && ((zt == 0 && on(2, 0)) || (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ && on(2, 1))));
+      if (FZ != 0 && ((zt == 0 && on(2, 0)) || (zt <= n2 - VZ && n2 - VZ < zt + 64 * VZ && on(2, 1)))) none = false;
     }
-  return nch * nty * BY * ntz * BZ - qx * qy * qz;
+    qz += none;
+  }
+  return nch * nty * ntz - qx * qy * qz;
 }
 
 // Whole-line z-edge stores allowed at z side s (HaloIOArgs::zh; -1: no
@@ -789,7 +821,8 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   constexpr int FXYZ = FEAT & (1 | 2 | 4 | 8 | 64 | 128);
   if (io.sync.my_flags && FXYZ != 0 && (FEAT & 2048) == 0 && !a.stamps && a.force_sel < 0) {
     a.sync = io.sync;
-    a.sync.feat_waves = hx_feature_waves<BY, RY, VZ, BZ, FEAT>(n0, n1, n2, a.ch, a.nty, a.ntz, io);
+    // counted per workgroup (step_sync_exit_wg)
+    a.sync.feat_waves = hx_feature_wgs<BY, RY, VZ, BZ, FEAT>(n0, n1, n2, a.ch, a.nty, a.ntz, io);
     if (a.sync.feat_waves < 1) a.sync.my_flags = nullptr;
   }
   if (io.sync_used) *io.sync_used = a.sync.my_flags != nullptr;

@@ -67,7 +67,9 @@ struct StepSync {
   int peer_rank[STEP_SYNC_MAX_PEERS] = {};
   int n_peers = 0, my_rank = 0;
   int64_t timeout_ticks = 0;
-  int64_t feat_waves = 0;  // exchanging waves of the launch (set by the launcher)
+  // counting units of the launch (set by the launcher): exchanging waves
+  // (acoustic kernel), or workgroups holding one (diffusion: step_sync_exit_wg)
+  int64_t feat_waves = 0;
   // Acquire after the wait (measurement knob IGG_STEP_SYNC_ACQUIRE): 2 system
   // (buffer_inv sc0 sc1, the default), 1 agent (buffer_inv sc1), 0 workgroup
   // (compiler ordering only; the kernel start invalidated the L1).
