@@ -11,6 +11,7 @@
 #         prof    [bench.py args]    rocprofv3 --kernel-trace --stats around bench.py
 #         profpy  script.py [args]   the same around any python script of the repo
 #         pmc     COUNTERS [bench.py args]   one rocprofv3 --pmc pass (COUNTERS comma-separated)
+#         pmcpy   COUNTERS script.py [args]  the same around any python script of the repo
 #   Logs go to gpurun_out/TAG/NN_KIND.log. Each step runs under its own
 #   `timeout -k 10` (default per kind, or KIND@SECONDS); the first failing step
 #   ends the script (no GPU step runs after a failure, a timeout or a fault).
@@ -44,6 +45,9 @@ for step in "$@"; do
     profpy)
       to=${to:-300}
       cmd=(rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof$i" -o run -- python3 "$R/${args[0]}" "${args[@]:1}") ;;
+    pmcpy)
+      to=${to:-120}
+      cmd=(rocprofv3 --pmc "${args[0]//,/ }" --output-format csv -d "$O/pmc$i" -o run -- python3 "$R/${args[1]}" "${args[@]:2}") ;;
     pmc)
       to=${to:-120}
       cmd=(rocprofv3 --pmc "${args[0]//,/ }" --output-format csv -d "$O/pmc$i" -o run -- python3 "$R/bench.py" "${args[@]:1}") ;;
@@ -52,7 +56,7 @@ for step in "$@"; do
   echo "== [$i] ${envs[*]} $kind ${args[*]} (timeout $to s) -> $log"
   (
     for e in "${envs[@]}"; do export "$e"; done
-    if [[ $kind == prof* || $kind == pmc ]]; then cd /tmp || exit 1; fi
+    if [[ $kind == prof* || $kind == pmc* ]]; then cd /tmp || exit 1; fi
     timeout -k 10 "$to" "${cmd[@]}"
   ) > "$log" 2>&1
   rc=$?
