@@ -3,8 +3,10 @@
 
 Metric (BASELINE.json): effective memory throughput T_eff = A_eff / t_it with
 A_eff = 3 * n_local * sizeof(T) (T read, Cp read, T2 written) per GPU, and the
-weak-scaling efficiency E(N) = t_it(1)/t_it(N) (computed by the driver from the
-per-N values).
+weak-scaling efficiency E(N) = t_it(1)/t_it(N). The driver computes E(N) from its
+own per-N runs; this script also measures it inside one job (``config.efficiency``:
+the 1-GPU run's local problem timed on the same ranks, interleaved with the real
+step in alternating order, so no box-to-box spread enters).
 
 ``value`` is the WHOLE-JOB aggregate T_eff (sum of the per-GPU T_eff over the
 N GPUs), as the bench contract prescribes; at N=1 it equals the per-GPU number.
@@ -312,8 +314,11 @@ def _all_ranks(comm, v: float) -> list:
 
 
 # Same-process weak-scaling efficiency (config.efficiency): interleaved pairs
-# of [the local problem, the multi-rank step], medians.
-EFF_PAIRS = 3
+# of [the local problem, the multi-rank step] in alternating order (even pairs
+# local first, odd pairs step first: a fixed order biased round 5's N=1 value
+# to 1.005 with a cold first local sample), after one untimed run of each form;
+# medians.
+EFF_PAIRS = 5
 LOCAL_GRAPH_STEPS = 10
 
 
@@ -394,36 +399,50 @@ def measure_efficiency(model, comm, log, graph: bool, k: int, pairs: int = EFF_P
         for _ in range(n):
             model.local_step()
 
-    tl, tm, own_l, own_m = [], [], [], []
-    for _ in range(pairs):
-        a, b = _timed_fn(run_local, comm, k)
-        tl.append(a)
-        own_l.append(b)
-        a, b = _timed_fn(model.run, comm, k)
-        tm.append(a)
-        own_m.append(b)
+    # one untimed run of each form first (graph upload, clocks, caches), so
+    # neither side's first sample is cold
+    run_local(k)
+    model.run(k)
+    tl, tm, own_l, own_m, order = [], [], [], [], []
+    for i in range(pairs):
+        first_local = i % 2 == 0
+        order.append("local,step" if first_local else "step,local")
+        for is_local in ((True, False) if first_local else (False, True)):
+            a, b = _timed_fn(run_local if is_local else model.run, comm, k)
+            (tl if is_local else tm).append(a)
+            (own_l if is_local else own_m).append(b)
     used_graph, gl = gl is not None, None
     _end_local_steps(model, saved)
     t_loc, t_step = _median(tl), _median(tm)
     per_rank_loc = _all_ranks(comm, _median(own_l))
     per_rank_step = _all_ranks(comm, _median(own_m))
     eff = t_loc / t_step if t_step > 0 else None
-    log(f"efficiency (same process, {pairs} interleaved pairs x {k} steps, medians): local "
-        f"{t_loc * 1e3:.4f} ms, step {t_step * 1e3:.4f} ms -> E = {eff:.4f}")
+    log(f"efficiency (same process, {pairs} pairs in alternating order x {k} steps, medians): local "
+        f"{t_loc * 1e3:.4f} ms [{min(tl) * 1e3:.4f}-{max(tl) * 1e3:.4f}], step {t_step * 1e3:.4f} ms "
+        f"[{min(tm) * 1e3:.4f}-{max(tm) * 1e3:.4f}] -> E = {eff:.4f}")
+
+    def _ms(xs):
+        return {"min": round(min(xs) * 1e3, 5), "median": round(_median(xs) * 1e3, 5),
+                "max": round(max(xs) * 1e3, 5)}
+
     return {
         "value": round(eff, 5) if eff is not None else None,
         "definition": "t_it(local problem) / t_it(step), same job: every rank times the identical local "
-                      "problem of the 1-GPU run (plain stencil, no exchange) interleaved with the real step; "
-                      "medians of the MAX over ranks",
+                      "problem of the 1-GPU run (plain stencil, no exchange) interleaved with the real step "
+                      "(pair order alternates, one untimed run of each first); medians of the MAX over ranks",
         "t_local_ms": round(t_loc * 1e3, 5),
         "t_step_ms": round(t_step * 1e3, 5),
+        "local_ms": _ms(tl),
+        "step_ms": _ms(tm),
         "pairs": pairs,
+        "pair_order": order,
         "steps": k,
         "local_ms_samples": [round(x * 1e3, 5) for x in tl],
         "step_ms_samples": [round(x * 1e3, 5) for x in tm],
         "per_rank_local_ms": [round(x * 1e3, 5) for x in per_rank_loc],
         "per_rank_step_ms": [round(x * 1e3, 5) for x in per_rank_step],
-        "per_rank_efficiency": [round(a / t_step, 5) if t_step > 0 else None for a in per_rank_loc],
+        # each rank's own local time over its own step time (both medians)
+        "per_rank_efficiency": [round(a / s, 5) if s > 0 else None for a, s in zip(per_rank_loc, per_rank_step)],
         "local_graph": used_graph,
     }
 

@@ -29,7 +29,10 @@ constexpr int64_t CHUNK = BLOCK * EPT;         // elements of a row per workgrou
 // a workgroup is 4 such waves (4 * GROWS outer rows).
 constexpr int GROWS = 8;
 
-struct alignas(16) B16 { uint64_t x, y; };
+// 16-B elements (complex128): a vector type, which stays in VGPRs; a struct
+// element of the GROWS-deep load array was kept in scratch (144 B per lane,
+// tools/kernel_resources.py).
+typedef uint64_t B16 __attribute__((ext_vector_type(2)));
 
 // Byte shift of the arena half selected by the device-resident epoch (odd ->
 // second half). The epoch lives in the uncached flag words, written by the

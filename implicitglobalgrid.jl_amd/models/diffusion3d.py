@@ -194,8 +194,13 @@ class Diffusion3D:
         # overtake this rank's own earlier writes - a switch into fused mode, a
         # restore, external edits: mark_modified).
         self._fentry = True
+        # Receive form of the last fused step (send-mode bits 4 / 64 / 16): where
+        # the primed halos live (arena, T's z halo column) and how the step
+        # synchronises. A step in another form re-primes first (_align_form).
+        self._fform = None
         self._graph_fused = None  # fused mode / step parity the graph was captured with
         self._graph_parity = 0
+        self._graph_cfg = None  # fused (variant, mode, rounds) of the capture
         self._graph_T = 0  # T's buffer when the graph was captured
 
     @property
@@ -355,15 +360,35 @@ class Diffusion3D:
         if self.fused:
             self._fh.drain(torch.cuda.current_stream().cuda_stream)
 
+    def _fused_step_mode(self) -> int:
+        # direct z (bit 4) needs the registered field buffers; where they
+        # could not be mapped (fields above the IPC limit) the same form runs
+        # with the arena z exchange
+        return self.fused_mode if self._fh.has_fields else self.fused_mode & ~4
+
+    def _align_form(self) -> None:
+        """Before a fused step: if the send mode's receive form changed since
+        the last primed step, re-prime. A primed step reads its halos where the
+        previous form's senders put them: the arena (arena z), T's z halo
+        column (direct z, bit 4; z unpack, bit 64, written by the previous
+        step's unpack copy) - a step of another form would read halos nobody
+        wrote (switching 8 -> 72 read a stale z column). So the
+        halos are materialised (update_halo_(T), collective: mode switches are
+        collective) and the next step reads them from T behind an entry
+        barrier (bit 16 changes how the neighbours' arrivals are counted)."""
+        form = self._fused_step_mode() & (4 | 16 | 64)
+        if self._fprimed and self._fform is not None and form != self._fform:
+            self.sync_halo()
+            self._fentry = True
+        self._fform = form
+
     def _step(self) -> None:
         T, T2, Cp = self.T, self.T2, self.Cp
         if self.fused:
             rd2 = [1.0 / self.dx ** 2, 1.0 / self.dy ** 2, 1.0 / self.dz ** 2]
             s = torch.cuda.current_stream().cuda_stream
-            # direct z (bit 4) needs the registered field buffers; where they
-            # could not be mapped (fields above the IPC limit) the same form
-            # runs with the arena z exchange
-            mode = self.fused_mode if self._fh.has_fields else self.fused_mode & ~4
+            self._align_form()  # (sync_halo leaves the buffer roles in place)
+            mode = self._fused_step_mode()
             if self.timer is not None:
                 with self.timer.phase("stencil+exchange"):
                     self._fh.step(T2.data_ptr(), T.data_ptr(), Cp.data_ptr(), rd2, self.dt * self.lam,
@@ -467,6 +492,8 @@ class Diffusion3D:
             raise RuntimeError("Diffusion3D.capture: hipGraphs need a GPU model")
         if not self._warm:
             self.step()
+        if self.fused:
+            self._align_form()  # no re-priming inside the capture
         if self.fused and not self._fprimed:
             self.step()  # captured fused steps read the arena: it must hold T's halos
         def record():
@@ -479,6 +506,7 @@ class Diffusion3D:
         self.graph = g
         self.graph_steps = steps
         self._graph_fused = self.fused
+        self._graph_cfg = self._fused_cfg()
         self._graph_parity = self._fstep % 2
         self._graph_T = self.T.data_ptr()
 
@@ -486,7 +514,7 @@ class Diffusion3D:
         """Advance ``nt`` steps (by graph replays of ``graph_steps`` steps if
         captured); in fused mode one exit barrier at the end (``_drain``)."""
         ran = nt > 0
-        if self.graph is not None and self._graph_fused == self.fused:
+        if self.graph is not None and self._graph_fused == self.fused and self._graph_cfg == self._fused_cfg():
             # The captured steps have their buffer roles baked in (T of the
             # capture is read first) and, fused, their arena halves too: they
             # assume a primed arena, no pending entry barrier and the
@@ -509,6 +537,11 @@ class Diffusion3D:
             self._step()
         if ran:
             self._drain()
+
+    def _fused_cfg(self):
+        """The fused kernel form a captured graph bakes in (a graph of another
+        form is not replayed: the steps run eagerly until the next capture)."""
+        return (self.fused_variant, self.fused_mode, self.fused_rounds) if self.fused else None
 
     def _graph_ready(self) -> bool:
         if self.T.data_ptr() != self._graph_T:

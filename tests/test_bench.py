@@ -168,10 +168,18 @@ def test_efficiency_measured_in_the_same_job(n):
     r, rec = _run(["--gpus", str(n), "--device", "cpu", "--n", "20", "--steps", "4", "--warmup", "1"])
     assert r.returncode == 0, r.stderr[-3000:]
     e = rec["config"]["efficiency"]
-    assert e is not None and e["pairs"] >= 3 and e["steps"] % 2 == 0
+    assert e is not None and e["pairs"] >= 5 and e["steps"] % 2 == 0
     assert len(e["local_ms_samples"]) == e["pairs"] == len(e["step_ms_samples"])
     assert abs(e["value"] - e["t_local_ms"] / e["t_step_ms"]) <= 1e-3 * e["value"] + 1e-4
     assert len(e["per_rank_local_ms"]) == n == len(e["per_rank_efficiency"])
+    # the pair order alternates (local-first in every pair
+    # biased the N=1 value), and min/median/max are reported for both forms
+    assert e["pair_order"] == ["local,step" if i % 2 == 0 else "step,local" for i in range(e["pairs"])]
+    for key in ("local_ms", "step_ms"):
+        assert e[key]["min"] <= e[key]["median"] <= e[key]["max"]
+    # per-rank efficiency: each rank's local time over its OWN step time
+    for a, s, x in zip(e["per_rank_local_ms"], e["per_rank_step_ms"], e["per_rank_efficiency"]):
+        assert abs(x - a / s) <= 1e-3 * x + 1e-4
 
 
 def test_nothing_between_warm_load_and_bracket():

@@ -188,6 +188,30 @@ def test_fused_loopback_graph_and_mode_switches(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_receive_form_switch_reprimes(gpu, graph):
+    """Switching the send mode's receive form mid-run (arena z 8 -> z unpack
+    72 -> direct z 12 -> in-kernel sync 88 -> 8) re-primes from the field: a
+    primed z-unpack step would otherwise read a z halo column no unpack wrote
+    (ADVICE r5). Bitwise against stencil + update_halo_ after every switch,
+    eager and with a capture after each switch."""
+    a, b = _pair((40, 36, 72), (1, 1, 1), torch.float64, 9, mode=8)
+    a.run(3)
+    b.run(3)
+    for mode in (72, 12, 88, 8):
+        b.fused_mode = mode
+        if graph:
+            b.capture(steps=2)
+        a.run(5)
+        b.run(5)
+        b.sync_halo()
+        torch.cuda.synchronize()
+        b.check()
+        assert torch.equal(a.T, b.T), mode
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
 def test_fused_arena_layout(gpu):
     """Region offsets are 256 B aligned and the z-face pitch covers n1-2 rows."""
     a, b = _pair((20, 37, 64), (1, 1, 1), torch.float64, 0)
