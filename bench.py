@@ -1259,6 +1259,10 @@ def main():
     os.environ.setdefault("IGG_PUT_TIMEOUT", "20")
     if args.share_gpu:
         os.environ.setdefault("IGG_TRANSPORT", "staged")
+    # The bench validates and A/B-times the transports itself (validate_transports,
+    # select_transport below): the library's own first-exchange choice
+    # (IGG_TRANSPORT=auto) stays out of the model setup before them.
+    os.environ.setdefault("IGG_TRANSPORT", "rccl")
     if "gather-pull" in EXCL:
         os.environ["IGG_GATHER_PULL"] = "0"
     me, dims, nprocs, coords, comm = igg.init_global_grid(

@@ -25,7 +25,7 @@ import torch  # noqa: E402
 import igg  # noqa: E402
 from igg._native import native  # noqa: E402
 
-PLAIN_OF = {50: 0, 55: 0, 41: 40, 42: 40, 44: 14, 45: 0}
+PLAIN_OF = {50: 0, 55: 0, 41: 40, 42: 40, 44: 14, 45: 0, 48: 9}
 
 
 def main():

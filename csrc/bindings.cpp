@@ -16,6 +16,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "igg/acoustic.hpp"
+#include "igg/coherence.hpp"
 #include "igg/comm.hpp"
 #include "igg/copy.hpp"
 #include "igg/fault.hpp"
@@ -28,6 +29,8 @@
 #include "igg/trace.hpp"
 
 namespace igg {
+void launch_zcol_probe(int dir, const void* src, void* dst, int64_t rows, int64_t pitch, int aux,
+                       hipStream_t stream);
 void launch_stream_probe(int kind, double* out, const double* a, const double* b, int64_t n, int blocks,
                          hipStream_t stream);
 }
@@ -400,15 +403,18 @@ PYBIND11_MODULE(_igg_native, m) {
   m.def("copy2d",
         [](const std::vector<std::tuple<uintptr_t, uintptr_t, int64_t, int64_t, int64_t, int64_t,
                                         int64_t, int64_t>>& cs,
-           int elem_bytes, bool device, uintptr_t stream) {
+           int elem_bytes, bool device, uintptr_t stream, bool system) {
           std::vector<Copy2D> v;
           for (const auto& c : cs)
             v.push_back({reinterpret_cast<const char*>(std::get<0>(c)),
                          reinterpret_cast<char*>(std::get<1>(c)), std::get<2>(c), std::get<3>(c),
                          std::get<4>(c), std::get<5>(c), std::get<6>(c), std::get<7>(c)});
-          if (device) launch_copy2d(v, elem_bytes, as_stream(stream));
+          if (device) launch_copy2d(v, elem_bytes, as_stream(stream), system);
           else host_copy2d(v, elem_bytes);
-        });
+        },
+        py::arg("copies"), py::arg("elem_bytes"), py::arg("device"), py::arg("stream") = 0,
+        py::arg("system") = false,
+        "Batched strided 2-D copies; system: the put transport's system-scope (sc0 sc1) stores.");
 
   // --- transports
   py::class_<Transport, std::shared_ptr<Transport>>(m, "Transport")
@@ -440,6 +446,20 @@ PYBIND11_MODULE(_igg_native, m) {
       .def("check_error", &PeerMesh::check_error)
       .def("clear_error", &PeerMesh::clear_error)
       .def("close", &PeerMesh::close);
+  py::class_<CoherenceProbe, std::shared_ptr<CoherenceProbe>>(m, "CoherenceProbe")
+      .def(py::init<std::shared_ptr<PeerMesh>, size_t>(), py::arg("mesh"), py::arg("bytes"),
+           "Collective over a 2-rank mesh (reader 0, writer 1): arenas of `bytes` (igg/coherence.hpp).")
+      .def("warm", [](CoherenceProbe& p, uintptr_t s) { p.warm(as_stream(s)); }, py::arg("stream"))
+      .def("write", [](CoherenceProbe& p, uint64_t v, bool in_kernel, uintptr_t s) { p.write(v, in_kernel, as_stream(s)); },
+           py::arg("value"), py::arg("in_kernel"), py::arg("stream"))
+      .def("check",
+           [](CoherenceProbe& p, uint64_t v, bool in_kernel, uintptr_t s) {
+             py::gil_scoped_release nogil;
+             return p.check(v, in_kernel, as_stream(s));
+           },
+           py::arg("value"), py::arg("in_kernel"), py::arg("stream"))
+      .def_property_readonly("workgroups", &CoherenceProbe::workgroups)
+      .def_property_readonly("words", &CoherenceProbe::words);
   py::class_<PutTransport, Transport, std::shared_ptr<PutTransport>>(m, "PutTransport")
       .def(py::init<std::shared_ptr<PeerMesh>>(), py::arg("mesh"))
       .def_property_readonly("mesh", &PutTransport::mesh_ptr);
@@ -583,6 +603,15 @@ PYBIND11_MODULE(_igg_native, m) {
     return v;
   });
   m.def("diffusion3d_variant_tile", &diffusion3d_variant_tile);
+  m.def("zcol_probe",
+        [](int dir, uintptr_t src, uintptr_t dst, int64_t rows, int64_t pitch, int aux, uintptr_t stream) {
+          launch_zcol_probe(dir, reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), rows, pitch, aux,
+                            as_stream(stream));
+        },
+        py::arg("dir"), py::arg("src"), py::arg("dst"), py::arg("rows"), py::arg("pitch"), py::arg("aux"),
+        py::arg("stream") = 0,
+        "z-face column probe: dir 0 pack (strided reads), 1 unpack (strided writes), 8-B elements; aux = cache "
+        "policy bits of the strided access (1 sc0, 2 nt, 16 sc1).");
   m.def("stream_probe", [](int kind, uintptr_t out, uintptr_t a, uintptr_t b, int64_t n, int blocks,
                            uintptr_t stream) {
     launch_stream_probe(kind, reinterpret_cast<double*>(out), reinterpret_cast<const double*>(a),

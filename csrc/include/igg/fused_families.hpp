@@ -40,10 +40,14 @@ bool fused_family_t11(const DiffusionArgs& d, const HaloIOArgs& io, int v, int m
 
 // tiling 9 (v4_by4_ry8) with the side-only z forms (ZSIDES: the 2x2x2
 // corner's best tiling, profiles/r4_shapes/ pass 4)
+// 48: tiling 9 with the DPP z-edge lane moves (ZDPP, round 6)
 template <typename T>
 bool fused_family_t9(const DiffusionArgs& d, const HaloIOArgs& io, int v, int mode, hipStream_t s) {
-  if (v != 9) return false;
-  launch_mode<T, 4, 8, 4, false, 1, ZSIDES>(d, io, mode, s);
+  switch (v) {
+    case 9: launch_mode<T, 4, 8, 4, false, 1, ZSIDES>(d, io, mode, s); break;
+    case 48: launch_mode<T, 4, 8, 4, false, 1, ZSIDES | ZDPP>(d, io, mode, s); break;
+    default: return false;
+  }
   return true;
 }
 

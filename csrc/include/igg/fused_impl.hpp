@@ -75,6 +75,49 @@ __device__ __forceinline__ T lane_read(T v, int l) {
   }
 }
 
+// DPP lane moves inside a 16-lane row (gfx9 row_shl / row_shr; ZDPP below):
+// lane i takes lane i + r (shl) or i - r (shr) of its own 16-lane row; lanes
+// whose source lies outside the row read 0 (bound_ctrl). r is a constant after
+// the row loop is unrolled (the switch folds); r = 0 is the identity.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+
+template <typename T, int CTRL>
+__device__ __forceinline__ T dpp_t(T v) {
+  if constexpr (sizeof(T) == 8) {
+    const int2 p = __builtin_bit_cast(int2, v);
+    return __builtin_bit_cast(T, make_int2(dpp_i<CTRL>(p.x), dpp_i<CTRL>(p.y)));
+  } else {
+    return __builtin_bit_cast(T, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+  }
+}
+
+#define IGG_DPP_ROW_CASES(BASE)                                                                                    \
+  case 1: return dpp_t<T, BASE + 1>(v);   case 2: return dpp_t<T, BASE + 2>(v);   case 3: return dpp_t<T, BASE + 3>(v);   \
+  case 4: return dpp_t<T, BASE + 4>(v);   case 5: return dpp_t<T, BASE + 5>(v);   case 6: return dpp_t<T, BASE + 6>(v);   \
+  case 7: return dpp_t<T, BASE + 7>(v);   case 8: return dpp_t<T, BASE + 8>(v);   case 9: return dpp_t<T, BASE + 9>(v);   \
+  case 10: return dpp_t<T, BASE + 10>(v); case 11: return dpp_t<T, BASE + 11>(v); case 12: return dpp_t<T, BASE + 12>(v); \
+  case 13: return dpp_t<T, BASE + 13>(v); case 14: return dpp_t<T, BASE + 14>(v); case 15: return dpp_t<T, BASE + 15>(v);
+
+template <typename T>
+__device__ __forceinline__ T row_shl(T v, int r) {  // lane i <- lane i + r
+  switch (r) {
+    IGG_DPP_ROW_CASES(0x100)
+    default: return v;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T row_shr(T v, int r) {  // lane i <- lane i - r
+  switch (r) {
+    IGG_DPP_ROW_CASES(0x110)
+    default: return v;
+  }
+}
+#undef IGG_DPP_ROW_CASES
+
 __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
   const int64_t q = nb / 8, r = nb % 8, xcd = b % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
@@ -171,6 +214,15 @@ constexpr int HZ = 262144;
 // slower in every shape, tiling 9 1.2 % faster at a 2x2x2 corner
 // (profiles/r4_shapes/, pass 4).
 constexpr int ZLO = 524288, ZHI = 1048576, ZSIDES = 2097152;
+// ZDPP (round 6): the z-edge lane moves as DPP row shifts
+// instead of v_readlane + select. The lane-distributed rows sit where one
+// shift reaches the edge lane within its 16-lane DPP row: low edge row r in
+// lane r (lane 0 <- lane r: row_shl r; send: lane r <- lane 0: row_shr r),
+// high edge row r in lane zh - r (lane zh <- lane zh - r: row_shr r; send:
+// lane zh - r <- lane zh: row_shl r). No SGPR round trip per row. Needs
+// RY <= 16, one z edge per wave, and zh % 16 >= RY - 1 (launch_mode checks;
+// otherwise the readlane form runs).
+constexpr int ZDPP = 4194304;
 
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT>
 __device__ __forceinline__ void
@@ -266,6 +318,8 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   // with it becomes a waterfall loop draining vmcnt (measured +27 % per step).
   const int zh = __builtin_amdgcn_readfirstlane(static_cast<int>((n2 - VZ - zt) / VZ));
   constexpr bool SLO = (FEAT & ZHI) == 0, SHI = (FEAT & ZLO) == 0;  // z sides this form handles
+  constexpr bool ZD = (FEAT & ZDPP) != 0;
+  static_assert(!ZD || (RY <= 16 && (FEAT & (4096 | 8192)) == 0), "ZDPP: RY <= 16, not with the LDS / edge-lane forms");
   const bool zin_lo = SLO && (FEAT & 4) && has_lo && zi0, zin_hi = SHI && (FEAT & 4) && has_hi && zi1;
   const bool zout_lo = SLO && (FEAT & 8) && has_lo && zo0, zout_hi = SHI && (FEAT & 8) && has_hi && zo1;
   const bool zin = zin_lo || zin_hi, zout = zout_lo || zout_hi;
@@ -273,15 +327,16 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   const bool hz_wave = (FEAT & HZ) != 0 && ((has_lo && a.zh_lo) || (has_hi && a.zh_hi));
   const int rl = lane & 31;
   // Lane-distributed z values: row r of the low edge in lane r, of the high
-  // edge in lane 32+r (rows < nv).
-  const bool lo_l = lane < 32 && rl < nv, hi_l = lane >= 32 && rl < nv;
+  // edge in lane 32+r (rows < nv); ZDPP: in lane zh - r.
+  const int rh = ZD ? zh - lane : rl;  // row of a high-edge lane
+  const bool lo_l = lane < 32 && rl < nv, hi_l = ZD ? (rh >= 0 && rh < nv) : (lane >= 32 && rl < nv);
   // Every lane loads (lanes without a row of their own read a valid dummy in
   // the same region): a load under a per-lane condition would be a divergent
   // branch around a load in the hot loop, which costs the loop its prefetch.
   const T* zsrc = lo_l && zin_lo ? zi0 + (y0 - 1) + rl
-                                 : (hi_l && zin_hi ? zi1 + (y0 - 1) + rl
+                                 : (hi_l && zin_hi ? zi1 + (y0 - 1) + rh
                                                    : (zin_lo ? zi0 : zi1) + (y0 - 1));
-  const int64_t zro = ((y0 - 1) + rl) * a.zrow;
+  const int64_t zro = ((y0 - 1) + (hi_l && !lo_l ? rh : rl)) * a.zrow;
   T* zdst = lo_l && zout_lo ? zo0 + zro : (hi_l && zout_hi ? zo1 + zro : nullptr);
   const bool remote = zout || yrow0 || yrow1 || (xs == 1 && xo0) || (xe == n0 - 1 && xo1);
   T znext = T(0), zv = T(0);
@@ -441,6 +496,15 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
       if constexpr (ZE && (FEAT & 4) != 0) {
         tc[r][0] = ze_lo ? zi_cur[r] : tc[r][0];
         tc[r][VZ - 1] = ze_hi ? zi_cur[r] : tc[r][VZ - 1];
+      } else if constexpr (ZD && (FEAT & 4) != 0) {
+        if constexpr (SLO) {
+          const T vl = row_shl(zcur, r);  // lane 0 <- lane r
+          tc[r][0] = pl ? vl : tc[r][0];
+        }
+        if constexpr (SHI) {
+          const T vh = row_shr(zcur, r);  // lane zh <- lane zh - r
+          tc[r][VZ - 1] = ph ? vh : tc[r][VZ - 1];
+        }
       } else if constexpr ((FEAT & 4) != 0 && (FEAT & 4096) == 0) {
         // z halo patch of row r right before its update, branch-free: patching
         // every row up front made the step wait for all of this plane's loads
@@ -520,6 +584,15 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
         } else if constexpr ((FEAT & 4096) != 0) {
           if (zout_lo && lane == 0) zs[2 * RY + r] = out[1];
           if (zout_hi && lane == zh) zs[3 * RY + r] = out[VZ - 2];
+        } else if constexpr (ZD && (FEAT & 8) != 0) {
+          if constexpr (SLO) {
+            const T vl = row_shr(out[1], r);  // lane r <- lane 0
+            zv = (zout_lo && lane == r) ? vl : zv;
+          }
+          if constexpr (SHI) {
+            const T vh = row_shl(out[VZ - 2], r);  // lane zh - r <- lane zh
+            zv = (zout_hi && lane == zh - r) ? vh : zv;
+          }
         } else if constexpr ((FEAT & 8) != 0) {
           // branch-free (see the z-in patch): unconditional readlanes + selects
           if constexpr (SLO) {
@@ -865,6 +938,15 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
 // XF: extra FEAT bits of the tiling (512 | 1024 for fused variant 40).
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, int XF = 0>
 void launch_mode(const DiffusionArgs& d, const HaloIOArgs& io, int mode, hipStream_t s) {
+  if constexpr ((XF & ZDPP) != 0) {
+    // the DPP z form: one z edge per wave, and the high edge's rows (lanes
+    // zh - r) inside the edge lane's 16-lane DPP row
+    const int64_t zh = ((d.n[2] - VZ) % (64 * VZ)) / VZ;
+    if (d.n[2] <= 64 * VZ + VZ || zh % 16 < RY - 1) {
+      launch_mode<T, BY, RY, VZ, PF, BZ, (XF & ~ZDPP)>(d, io, mode, s);
+      return;
+    }
+  }
   if constexpr ((XF & 8192) != 0) {
     // the edge-lane z form needs every wave to hold at most one z edge
     if (d.n[2] <= 64 * VZ + VZ) {

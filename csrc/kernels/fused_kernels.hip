@@ -93,7 +93,7 @@ bool diffusion3d_fused_variant_ok(int v) {
 #ifdef IGG_PROBES
   if (v == 2 || v == 11 || v == 41 || v == 45) return true;
 #endif
-  return v == 0 || v == 9 || v == 14 || v == 40 || v == 42 || v == 44 || v == 50;
+  return v == 0 || v == 9 || v == 14 || v == 40 || v == 42 || v == 44 || v == 48 || v == 50;
 }
 
 void launch_diffusion3d_fused(const DiffusionArgs& a, const HaloIOArgs& io, int variant, int mode,

@@ -2,6 +2,7 @@
 // MI355X-specific replacement of the reference's MPI point-to-point layer
 // (update_halo.jl:713-753); no counterpart exists in the reference.
 #include "igg/peer.hpp"
+#include "igg/fault.hpp"
 
 #include "igg/ipc.hpp"
 
@@ -107,6 +108,7 @@ void PeerMesh::exchange_handles(bool flags_too) {
   const size_t hb = sizeof(hipIpcMemHandle_t);
   std::string error;
   try {
+    inject_fail("peer_map");  // tests: a rank that cannot map its peers (IGG_INJECT_FAIL)
     for (int r = 0; r < nranks_; ++r) {
       if (r == rank_) continue;
       const std::string& h = all[r];

@@ -32,7 +32,7 @@ def compiled_variants() -> list[int]:
     return [v for v in range(len(variants())) if native.diffusion3d_variant_compiled(v)]
 
 
-FUSED_VARIANTS = (0, 2, 9, 11, 14, 40, 41, 42, 44, 45, 50)
+FUSED_VARIANTS = (0, 2, 9, 11, 14, 40, 41, 42, 44, 45, 48, 50)
 
 
 def compiled_fused_variants() -> list[int]:

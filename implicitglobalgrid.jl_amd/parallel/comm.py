@@ -244,6 +244,8 @@ class Communicator:
         if self.size == 1:
             return None
         choice = config.transport_choice() if choice is None else choice
+        if choice == "auto":  # no selection here (parallel/halo.py chooses per field set): RCCL
+            choice = "rccl"
         if choice not in ("rccl", "torch", "staged", "put"):
             raise IGGError(f"unknown device transport {choice!r}")
         if choice == "staged":

@@ -92,7 +92,7 @@ def gather_(A: torch.Tensor, A_global: torch.Tensor | None, *, root: int = 0) ->
         if _pull_ok(gg, A):
             _gather_pull(A, A_global, root, s, dims, me, nprocs, c)
             return
-    if A.is_cuda and nprocs > 1 and c.rccl is None and gg.amdgpu_enabled and config.transport_choice() == "rccl":
+    if A.is_cuda and nprocs > 1 and c.rccl is None and gg.amdgpu_enabled and config.transport_choice() in ("rccl", "auto"):
         c.ensure_rccl()
     if A.is_cuda and (nprocs == 1 or c.rccl is not None):
         _gather_device(A, A_global, root, s, dims, me, nprocs, c)

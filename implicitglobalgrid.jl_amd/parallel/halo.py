@@ -31,6 +31,15 @@ _MAX_PLANS = 512
 # evictions (a rank that tuned alone would pair its extra exchanges with the
 # other ranks' normal ones).
 _sig_modes: dict = {}
+# IGG_TRANSPORT=auto (the default; off after an explicit set_transport): the
+# device transport by the same field-set signature, chosen on the signature's
+# first eager device exchange (transport_select.auto_select: bitwise against
+# the host-staged exchange, timed, collective) and switched to per call.
+_auto = False
+_selecting = False  # inside a selection: its own probe exchanges use the transport as set
+_sig_transport: dict = {}
+_transport_log: list = []
+_cur_transport = None  # name of the device transport the engine holds (None: pending / none)
 _buf_dtype = {False: None, True: None}
 _debug_sync = False
 _graphs: list = []  # weakrefs to hipGraphs that captured update_halo_
@@ -124,7 +133,7 @@ def set_halo_mode(mode: str) -> None:
     """Select the exchange schedule: 'sequential' (x->y->z faces, the reference
     algorithm), 'onephase' (faces+edges+corners in one phase) or 'auto'."""
     _grid.check_initialized()
-    if mode == "onephase" and _loopback_one_sided and _loopback_comm is not None and _loopback_comm.name == "rccl":
+    if mode == "onephase" and _loopback_one_sided and "rccl" in _loopback_comms:
         raise IGGError(_ONE_SIDED_ONEPHASE)
     _engine.set_mode(HALO_MODES[mode])
     _sig_modes.clear()
@@ -166,6 +175,11 @@ def _init_engine(gg) -> None:
         _engine.set_pack_mode(d, config.PACK_MODES.index(m))
     _debug_sync = config.debug_sync()
     _set_poll_every(config.poll_every())
+    global _auto, _cur_transport
+    _auto = gg.nprocs > 1 and bool(gg.amdgpu_enabled) and config.transport_choice() == "auto"
+    _sig_transport.clear()
+    _transport_log.clear()
+    _cur_transport = None
     if gg.nprocs > 1:
         _engine.set_transport(gg.comm.host_transport(), False)
         # The device transport (RCCL communicator, put mesh) is created by the
@@ -177,7 +191,7 @@ def _init_engine(gg) -> None:
 
 
 _dev_pending = False
-_PENDING_NAMES = {"rccl": "rccl", "put": "put", "staged": "gloo-staged", "torch": "torch-nccl"}
+_PENDING_NAMES = {"rccl": "rccl", "put": "put", "staged": "gloo-staged", "torch": "torch-nccl", "auto": "auto"}
 
 
 def _set_dev_pending(flag: bool) -> None:
@@ -187,11 +201,74 @@ def _set_dev_pending(flag: bool) -> None:
 
 def _ensure_device_transport() -> None:
     """Create the configured device transport on first use (collective: every
-    rank's first device exchange happens at the same point)."""
+    rank's first device exchange happens at the same point). With
+    IGG_TRANSPORT=auto this is the transport of exchanges that are not
+    selected (a field set first seen inside a hipGraph capture): RCCL, or the
+    host-staged transport where ranks share a GPU (RCCL refuses that); the
+    selection of the first eager exchange replaces it."""
     global _dev_pending
     if _dev_pending:
         _dev_pending = False
-        _engine.set_transport(_grid.global_grid().comm.device_transport(), True)
+        choice = config.transport_choice()
+        if choice == "auto":
+            from .transport_select import _shared_device
+
+            choice = "staged" if _shared_device(_grid.global_grid().comm) else "rccl"
+        use_transport(choice)
+
+
+def use_transport(name: str) -> None:
+    """Point the engine at device transport ``name`` without ending the
+    automatic choice (internal: IGG_TRANSPORT=auto selection and per-signature
+    switches; the schedule caches stay, they are per signature too).
+    Collective on first use of a transport (creates it)."""
+    global _cur_transport
+    name = {v: k for k, v in _PENDING_NAMES.items()}.get(name, name)
+    if _loopback_comm is not None:
+        _use_loopback(name)
+    else:
+        _engine.set_transport(_grid.global_grid().comm.device_transport(name), True)
+    _set_dev_pending(False)
+    _cur_transport = name
+
+
+class selecting:
+    """Context of a transport selection: the probe exchanges inside use the
+    transport as set (no nested automatic selection)."""
+
+    def __enter__(self):
+        global _selecting
+        self._prev, _selecting = _selecting, True
+        return self
+
+    def __exit__(self, *exc):
+        global _selecting
+        _selecting = self._prev
+        return False
+
+
+def tuned_transports() -> list:
+    """IGG_TRANSPORT=auto selections so far: one record per field-set
+    signature (shapes, dtype, per-candidate check outcome and ms per exchange,
+    the chosen transport)."""
+    return list(_transport_log)
+
+
+def auto_transport() -> bool:
+    """Whether update_halo_ chooses the device transport itself (IGG_TRANSPORT=auto)."""
+    return _auto
+
+
+def meshes() -> list:
+    """The put transport's peer meshes of this grid (multi-rank and loopback)."""
+    out = []
+    gg = _grid.global_grid()
+    if gg.comm is not None and getattr(gg.comm, "mesh", None) is not None:
+        out.append(gg.comm.mesh)
+    for c in _loopback_comms.values():
+        if hasattr(c, "mesh"):
+            out.append(c.mesh)
+    return out
 
 
 _poll_every = 1000
@@ -203,10 +280,13 @@ def _set_poll_every(n: int) -> None:
 
 
 def _drop_engine() -> None:
-    global _engine, _loopback_comm, _loopback_one_sided
+    global _engine, _loopback_comm, _loopback_one_sided, _auto, _cur_transport
     _release_graphs()
     _plans.clear()
     _sig_modes.clear()
+    _sig_transport.clear()
+    _loopback_comms.clear()
+    _auto, _cur_transport = False, None
     if _engine is not None:
         _engine.pool_free()
     _engine = None
@@ -218,15 +298,21 @@ def _drop_engine() -> None:
 def set_transport(name: str) -> None:
     """Switch the device transport of ``update_halo_`` ('rccl', 'put', 'torch'
     or 'staged'). Collective: every rank must switch at the same point (the
-    first use of a transport creates its communicator / peer mesh)."""
+    first use of a transport creates its communicator / peer mesh). An
+    explicit choice: update_halo_ stops choosing by itself (IGG_TRANSPORT=auto)."""
+    global _auto, _cur_transport
     name = {v: k for k, v in _PENDING_NAMES.items()}.get(name, name)  # transport_name() spellings too
     gg = _grid.global_grid()
     if gg.nprocs == 1:
         raise IGGError("set_transport: a single-process grid has no device transport")
     if not gg.amdgpu_enabled:
         raise IGGError("set_transport: the grid was not initialised for GPU fields")
+    if name == "auto":
+        raise IGGError("set_transport: 'auto' is the IGG_TRANSPORT default, not a transport")
     _engine.set_transport(gg.comm.device_transport(name), True)
     _set_dev_pending(False)
+    _auto, _cur_transport = False, name
+    _sig_transport.clear()
     _sig_modes.clear()
     for p in _plans.values():
         p[3] = None  # schedule costs differ per transport: 'auto' measures again
@@ -244,17 +330,11 @@ def check_transport() -> None:
     """Raise if a put-transport synchronisation kernel timed out (its spin
     waits are bounded; a timeout means some exchange's halo is invalid) or an
     RCCL communicator reported an asynchronous error."""
-    meshes = []
-    gg = _grid.global_grid()
-    if gg.comm is not None and getattr(gg.comm, "mesh", None) is not None:
-        meshes.append(gg.comm.mesh)
-    if _loopback_comm is not None and hasattr(_loopback_comm, "mesh"):
-        meshes.append(_loopback_comm.mesh)
-    for m in meshes:
+    for m in meshes():
         m.check_error()
+    gg = _grid.global_grid()
     rcc = [getattr(gg.comm, "rccl", None) if gg.comm is not None else None]
-    if _loopback_comm is not None and isinstance(_loopback_comm, native.RcclComm):
-        rcc.append(_loopback_comm)
+    rcc += [c for c in _loopback_comms.values() if isinstance(c, native.RcclComm)]
     for c in rcc:
         if c is not None:
             c.check_async_error()  # ncclCommGetAsyncError: raises on an asynchronous RCCL failure
@@ -262,11 +342,12 @@ def check_transport() -> None:
 
 def abort_loopback() -> None:
     """Abort the single-GPU loopback RCCL communicator (bounded-wait expiry)."""
-    if _loopback_comm is not None and isinstance(_loopback_comm, native.RcclComm):
-        try:
-            _loopback_comm.abort()
-        except Exception:
-            pass
+    for c in _loopback_comms.values():
+        if isinstance(c, native.RcclComm):
+            try:
+                c.abort()
+            except Exception:
+                pass
 
 
 # Device transports whose exchanges can be recorded in a hipGraph: RCCL
@@ -283,7 +364,8 @@ def capturable() -> bool:
         return _engine.transport_name(True) in CAPTURABLE
     if _grid.global_grid().nprocs == 1:
         return True
-    return transport_name() in CAPTURABLE
+    # pending auto: the first exchange creates RCCL (or staged where ranks share a GPU)
+    return transport_name() in CAPTURABLE + ("auto",)
 
 
 def capture_graph(record, what: str, uses_halo: bool = True):
@@ -326,6 +408,10 @@ def sync_grid() -> None:
 
 
 _loopback_comm = None
+# Loopback transports by kind ('rccl', 'put'): one with IGG_TRANSPORT=rccl|put,
+# both with auto (kept alive side by side: replacing one destroyed it
+# mid-process, round 5); _loopback_comm is the one the engine holds.
+_loopback_comms: dict = {}
 # Loopback emulation of a shape with one side in some dim (a node's edge or
 # corner rank): one process plays every neighbour through ONE self-peer, so
 # RCCL pairs messages by issue order alone. The sequential schedule issues one
@@ -359,37 +445,65 @@ def enable_loopback(dims=(True, True, True)) -> None:
     if gg.nprocs != 1 or not gg.amdgpu_enabled:
         raise IGGError("loopback mode needs a single-process grid with a GPU")
     sides = [(bool(x[0]), bool(x[1])) if isinstance(x, (tuple, list)) else (bool(x), bool(x)) for x in dims]
+    nb = gg.neighbors.tolist()  # the grid's table changes only once every check passed
     for d in range(NDIMS):
         for s in range(2):
             if sides[d][s]:
-                gg.neighbors[s, d] = 0
-    dims = [any(sd) for sd in sides]
-    _loopback_one_sided = any(sd[0] != sd[1] for sd in sides)
-    want = "put" if config.transport_choice() == "put" else "rccl"
-    # A later call (another emulated shape) reuses the loopback transport of
-    # the same kind instead of replacing it: a replaced RCCL communicator or
-    # put mesh is destroyed mid-process, and a put -> RCCL switch that way was
-    # followed by a GPU memory fault (round 5, benchmarks/rank_shapes.py).
-    if _loopback_comm is None or _loopback_comm.name != want:
-        if _loopback_comm is not None:
-            raise IGGError(f"loopback mode: the '{_loopback_comm.name}' loopback transport exists; one transport "
-                           f"kind per process (IGG_TRANSPORT={want} requested)")
-        if want == "put":
-            _loopback_comm = native.PutTransport(native.PeerMesh(0, 1, lambda b: [bytes(b)]))
-        else:
-            _loopback_comm = native.RcclComm(native.RcclComm.unique_id(), 1, 0)
-    nb = gg.neighbors.tolist()
+                nb[s][d] = 0
+    one_sided = any(sd[0] != sd[1] for sd in sides)
+    global _auto
+    choice = config.transport_choice()
+    kinds = ("rccl", "put") if choice == "auto" else (("put",) if choice == "put" else ("rccl",))
+    if one_sided and _engine.mode == HALO_MODES["onephase"]:
+        if choice == "auto":
+            kinds = ("put",)  # the only loopback transport that pairs one-sided one-phase messages
+        elif "rccl" in kinds:
+            raise IGGError(_ONE_SIDED_ONEPHASE)  # before the grid or the engine changes
+    want = kinds[0]
+    # A later call (another emulated shape) reuses the loopback transports
+    # instead of replacing them: a replaced RCCL communicator or put mesh is
+    # destroyed mid-process, and a put -> RCCL switch that way was followed
+    # by a GPU memory fault (round 5, benchmarks/rank_shapes.py).
+    for k in kinds:
+        if k not in _loopback_comms and _loopback_comms and choice != "auto":
+            raise IGGError(f"loopback mode: the '{next(iter(_loopback_comms))}' loopback transport exists; one "
+                           f"transport kind per process (IGG_TRANSPORT={k} requested)")
+        if k not in _loopback_comms:
+            _loopback_comms[k] = (native.PutTransport(native.PeerMesh(0, 1, lambda b: [bytes(b)])) if k == "put"
+                                  else native.RcclComm(native.RcclComm.unique_id(), 1, 0))
+    _loopback_comm = _loopback_comms[want]
+    _auto = choice == "auto"
+    _sig_transport.clear()
     # one-phase directions (k = 9*cx + 3*cy + cz, c = 0 low / 1 none / 2 high):
     # a peer where every non-zero component points at an emulated side
     peers = [0 if all(c == 1 or sides[d][c // 2] for d, c in enumerate((k // 9, (k // 3) % 3, k % 3)))
              else PROC_NULL for k in range(27)]
     peers[13] = 1
+    _loopback_one_sided = one_sided
+    for s_ in range(2):
+        for d in range(NDIMS):
+            gg.neighbors[s_, d] = nb[s_][d]
     _engine.set_grid(native.GridInfo(1, 2, gg.nxyz.tolist(), gg.overlaps.tolist(), nb, peers))
     _engine.set_transport(_loopback_comm, True)
-    if _loopback_one_sided and want == "rccl" and _engine.mode == HALO_MODES["onephase"]:
-        raise IGGError(_ONE_SIDED_ONEPHASE)
+    global _cur_transport
+    _cur_transport = want
     _plans.clear()
     _sig_modes.clear()
+
+
+def loopback_active() -> bool:
+    """The single-GPU loopback emulation is on (enable_loopback)."""
+    return _loopback_comm is not None
+
+
+def _use_loopback(name: str) -> None:
+    global _loopback_comm
+    if name not in _loopback_comms:
+        raise IGGError(f"loopback mode: no '{name}' loopback transport in this process")
+    if name == "rccl" and _loopback_one_sided and _engine.mode == HALO_MODES["onephase"]:
+        raise IGGError(_ONE_SIDED_ONEPHASE)
+    _loopback_comm = _loopback_comms[name]
+    _engine.set_transport(_loopback_comm, True)
 
 
 # --- argument checks (update_halo.jl:804-834) ---------------------------------
@@ -554,8 +668,22 @@ def update_halo_(*fields) -> None:
     if device and _dev_pending:
         _ensure_device_transport()
     stream = torch.cuda.current_stream().cuda_stream if device else 0
-    if mode is None and device and _engine.mode == HALO_MODES["auto"]:
+    sig = None
+    if device and _auto and not _selecting:
+        # IGG_TRANSPORT=auto: this signature's transport (chosen on its first
+        # eager exchange that reaches another rank; collective)
         sig = tuple((tuple(A.shape), tuple(A.stride()), A.dtype) for A in fields)
+        name = _sig_transport.get(sig)
+        if name is None and _remote_peers() and not torch.cuda.is_current_stream_capturing():
+            from .transport_select import auto_select
+
+            name, rec = auto_select(fields)
+            _sig_transport[sig] = name
+            _transport_log.append(rec)
+        if name is not None and name != _cur_transport:
+            use_transport(name)
+    if mode is None and device and _engine.mode == HALO_MODES["auto"]:
+        sig = sig or tuple((tuple(A.shape), tuple(A.stride()), A.dtype) for A in fields)
         mode = p[3] = _sig_modes.get(sig)
         if mode is None and _remote_peers() and _engine.transport_name(True) != "put" \
                 and not torch.cuda.is_current_stream_capturing():

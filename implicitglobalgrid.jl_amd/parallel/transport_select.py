@@ -8,13 +8,21 @@ and trusts the answer. Here the device transports differ in speed by node
 rank shape (RCCL p2p groups vs the IPC put transport: 1.098 vs 1.046 x the
 plain step at a 2x2x2 corner rank, profiles/r5_update_halo/) and the put
 transport's correctness rests on cross-device coherence of the node it runs
-on. So ``select_transport`` measures both on the node: the same probe check
-``bench.py`` runs before and after its timed region, as a library call.
+on. So the choice is measured on the node:
+
+* ``select_transport(A)``: explicit library call (the same probe check
+  ``bench.py`` runs before and after its timed region);
+* ``auto_select(fields)``: what ``update_halo_`` runs by itself on the first
+  eager device exchange of a field-set signature when ``IGG_TRANSPORT=auto``
+  (the default): same check, probe shaped like the call's fields, winner cached
+  per signature (parallel/halo.py).
 """
 from __future__ import annotations
 
+import math
 import socket
 import time
+import warnings
 
 import torch
 
@@ -25,23 +33,105 @@ from . import halo as _halo
 DEFAULT_CANDIDATES = ("put", "rccl")
 
 
-def _probe(A: torch.Tensor, rank: int) -> torch.Tensor:
-    """Rank-distinct payload of A's shape and dtype, exact in every dtype the
-    halo engine moves (integer-valued and small), boundary planes poisoned:
-    a missing, misplaced or wrong-rank receive changes the result."""
+def _exact_limit(dtype: torch.dtype) -> int:
+    """Integers 0..limit-1 are exact (and distinct) in ``dtype``."""
+    if dtype.is_complex:
+        dtype = {torch.complex32: torch.float16, torch.complex64: torch.float32}.get(dtype, torch.float64)
+    if dtype == torch.bool:
+        return 2
+    if dtype.is_floating_point:  # 2 ** (mantissa bits + 1): eps = 2 ** -mantissa bits
+        return 1 << (round(-math.log2(torch.finfo(dtype).eps)) + 1)
+    return int(torch.iinfo(dtype).max) + 1
+
+
+def _probe(A: torch.Tensor, rank: int, nranks: int = 1) -> torch.Tensor:
+    """Rank-distinct payload of A's shape and dtype, boundary planes poisoned
+    with 0: a missing, misplaced or wrong-rank receive changes the result.
+    Rank r's values lie in [(r+1)*span, (r+2)*span), all exact and distinct in
+    the dtype (float16: 2048 integers, bfloat16: 256, uint8: 256), so 0 is in
+    no rank's range and neighbouring positions never round together."""
     n = A.numel()
-    span = max(2, min(n, 1 << 11))
+    limit = min(_exact_limit(A.dtype), 1 << 53)
+    span = max(1, min(n, 1 << 11, limit // (max(1, nranks) + 1)))
     v = (torch.arange(n, device=A.device, dtype=torch.int64) % span) + (rank + 1) * span
     X = v.to(A.dtype).view(A.shape).clone()
     for d in range(A.dim()):
         if A.shape[d] > 1:
-            X.select(d, 0).fill_(-7)
-            X.select(d, A.shape[d] - 1).fill_(-7)
+            X.select(d, 0).fill_(0)
+            X.select(d, A.shape[d] - 1).fill_(0)
     return X
 
 
 def _agree_max(comm, v: float) -> float:
-    return float(comm.allreduce(float(v), op="max")) if comm.size > 1 else float(v)
+    return float(comm.allreduce(float(v), op="max")) if comm is not None and comm.size > 1 else float(v)
+
+
+def _check_and_time(fields, names, switch, comm, rank: int, nranks: int, ref, steps: int,
+                    skip: dict | None = None) -> tuple[dict, dict]:
+    """For each transport name: ``switch(name)`` (collective), one
+    ``update_halo_`` of probes shaped like ``fields``, compared with ``ref``
+    (the probes after the reference exchange; None: every candidate must equal
+    the first one that passed), then ``steps`` timed exchanges (MAX over
+    ranks). Every outcome is agreed over ranks. Returns (checked, ms)."""
+    checked, ms = {}, {}
+    first_ok = None
+    for name in names:
+        if skip and name in skip:
+            checked[name] = skip[name]
+            continue
+        why = ""
+        X = None
+        try:
+            switch(name)  # collective; creates the communicator / peer mesh
+            X = [_probe(A, rank, nranks) for A in fields]
+        except Exception as e:  # e.g. RCCL refuses ranks that share a GPU
+            why = f"{type(e).__name__}: {e}"[:300]
+        if _agree_max(comm, 1.0 if why else 0.0) == 0:  # every rank has its probes: exchange
+            try:
+                _halo.update_halo_(*X)
+                torch.cuda.synchronize()
+                _halo.check_transport()
+                want = ref if ref is not None else first_ok
+                if want is not None:
+                    for x, r in zip(X, want):
+                        if not torch.equal(x, r):
+                            bad = (x != r).nonzero()
+                            why = f"mismatch in {bad.shape[0]} elements, first {bad[:4].tolist()}"
+                            break
+            except Exception as e:
+                why = f"{type(e).__name__}: {e}"[:300]
+            if _agree_max(comm, 1.0 if why else 0.0) > 0 and not why:
+                why = "failed on another rank"
+            if why:
+                for m in _halo.meshes():
+                    m.clear_error()  # a timed-out put sync leaves a sticky error word
+        elif not why:
+            why = "failed on another rank"
+        checked[name] = why or "ok"
+        if why:
+            continue
+        if ref is None and first_ok is None:
+            first_ok = [x.clone() for x in X]
+        # timing: the probes again (the caller's fields stay untouched)
+        _halo.update_halo_(*X)
+        torch.cuda.synchronize()
+        if comm is not None:
+            comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(max(1, int(steps))):
+            _halo.update_halo_(*X)
+        torch.cuda.synchronize()
+        dt = _agree_max(comm, time.perf_counter() - t0)
+        ms[name] = round(dt / max(1, int(steps)) * 1e3, 5)
+        del X
+    return checked, ms
+
+
+def _shared_device(comm) -> bool:
+    """Some ranks share a GPU (RCCL and torch's NCCL group refuse that). Collective."""
+    me_dev = (socket.gethostname(), int(torch.cuda.current_device()))
+    devs = comm.all_gather_object(me_dev)
+    return len(set(devs)) < len(devs)
 
 
 def select_transport(A: torch.Tensor, candidates=DEFAULT_CANDIDATES, steps: int = 10,
@@ -58,8 +148,9 @@ def select_transport(A: torch.Tensor, candidates=DEFAULT_CANDIDATES, steps: int 
     allocated while this runs. Returns ``{"checked": {name: "ok" | reason},
     "ms": {name: ms per exchange}, "chosen": name}``; on a single-process or
     CPU grid nothing is switched and ``chosen`` is the current transport.
-    Raises IGGError if no candidate passes (the previous transport is then
-    restored where it still works)."""
+    An explicit choice: ``update_halo_`` no longer selects by itself
+    (IGG_TRANSPORT=auto) afterwards. Raises IGGError if no candidate passes
+    (the previous transport is then restored where it still works)."""
     gg = _grid.global_grid()
     _grid.check_initialized()
     out = {"checked": {}, "ms": {}, "chosen": _halo.transport_name()}
@@ -68,57 +159,18 @@ def select_transport(A: torch.Tensor, candidates=DEFAULT_CANDIDATES, steps: int 
         return out
     comm = gg.comm
     before = _halo.transport_name()
-    # RCCL (and torch's NCCL group) refuse ranks that share a device
-    me_dev = (socket.gethostname(), int(torch.cuda.current_device()))
-    devs = comm.all_gather_object(me_dev)
-    shared = len(set(devs)) < len(devs)
-    # reference: the host-staged exchange (the reference's non-GPU-aware path)
-    _halo.set_transport("staged")
-    R = _probe(A, int(gg.me))
-    _halo.update_halo_(R)
-    torch.cuda.synchronize()
-    for name in candidates:
-        why = ""
-        X = None
-        if shared and name in ("rccl", "torch"):
-            out["checked"][name] = "skipped: ranks share a GPU (RCCL refuses duplicate devices)"
-            continue
-        try:
-            _halo.set_transport(name)  # collective; creates the communicator / peer mesh
-            X = _probe(A, int(gg.me))
-        except Exception as e:  # e.g. RCCL refuses ranks that share a GPU
-            why = f"{type(e).__name__}: {e}"[:300]
-        if _agree_max(comm, 1.0 if why else 0.0) == 0:  # every rank has its probe: exchange
-            try:
-                _halo.update_halo_(X)
-                torch.cuda.synchronize()
-                _halo.check_transport()
-                if not torch.equal(X, R):
-                    bad = (X != R).nonzero()
-                    why = f"mismatch in {bad.shape[0]} elements, first {bad[:4].tolist()}"
-            except Exception as e:
-                why = f"{type(e).__name__}: {e}"[:300]
-            if _agree_max(comm, 1.0 if why else 0.0) > 0 and not why:
-                why = "failed on another rank"
-            if why and getattr(comm, "mesh", None) is not None:
-                comm.mesh.clear_error()  # a timed-out put sync leaves a sticky error word
-        elif not why:
-            why = "failed on another rank"
-        out["checked"][name] = why or "ok"
-        if why:
-            continue
-        # timing: the probe again (A stays untouched), MAX over ranks
-        _halo.update_halo_(X)
+    shared = _shared_device(comm)
+    with _halo.selecting():
+        # reference: the host-staged exchange (the reference's non-GPU-aware path)
+        _halo.set_transport("staged")
+        R = _probe(A, int(gg.me), int(gg.nprocs))
+        _halo.update_halo_(R)
         torch.cuda.synchronize()
-        comm.barrier()
-        t0 = time.perf_counter()
-        for _ in range(max(1, int(steps))):
-            _halo.update_halo_(X)
-        torch.cuda.synchronize()
-        dt = _agree_max(comm, time.perf_counter() - t0)
-        out["ms"][name] = round(dt / max(1, int(steps)) * 1e3, 5)
-        del X
-    del R
+        skip = {n: "skipped: ranks share a GPU (RCCL refuses duplicate devices)"
+                for n in candidates if shared and n in ("rccl", "torch")}
+        out["checked"], out["ms"] = _check_and_time([A], list(candidates), _halo.set_transport, comm, int(gg.me),
+                                                    int(gg.nprocs), [R], steps, skip)
+        del R
     ok = [n for n in candidates if out["checked"].get(n) == "ok"]
     if not ok:
         try:
@@ -130,3 +182,62 @@ def select_transport(A: torch.Tensor, candidates=DEFAULT_CANDIDATES, steps: int 
     _halo.set_transport(best)
     out["chosen"] = _halo.transport_name()
     return out
+
+
+# auto_select: timed exchanges per candidate (after one untimed warm-up each)
+AUTO_STEPS = 5
+
+
+def auto_select(fields) -> tuple[str, dict]:
+    """IGG_TRANSPORT=auto: the device transport for this field set, chosen on
+    the first eager device exchange of its signature (collective: every rank
+    makes the same update_halo_ calls on the same local shapes).
+
+    * ranks on several nodes: 'rccl' (IPC peer mappings need one node);
+    * one node: 'put' and 'rccl' (not where ranks share a GPU: RCCL refuses
+      duplicate devices) are each checked bitwise against the host-staged
+      exchange of probes shaped like ``fields`` and timed; the fastest that
+      passed wins. None passed: 'staged' (always correct, slow), with a warning;
+    * loopback emulation (one process, every neighbour itself): 'put' and
+      'rccl' loopback transports, checked against each other (there is no
+      second rank for a host-staged reference) and timed; a disagreement keeps
+      'rccl', the loopback's former default.
+
+    The caller's fields are not modified. Returns (name, record)."""
+    gg = _grid.global_grid()
+    rec = {"shapes": [tuple(A.shape) for A in fields], "dtype": str(fields[0].dtype), "checked": {}, "ms": {}}
+    with _halo.selecting():
+        if _halo.loopback_active():
+            rec["checked"], rec["ms"] = _check_and_time(fields, ["rccl", "put"], _halo.use_transport, None, 0, 1,
+                                                        None, AUTO_STEPS)
+            ok = [n for n in ("rccl", "put") if rec["checked"].get(n) == "ok"]
+            if rec["checked"].get("put", "").startswith("mismatch"):
+                warnings.warn(f"update_halo_ (IGG_TRANSPORT=auto, loopback): put and rccl disagree; keeping rccl "
+                              f"({rec['checked']['put']})")
+                ok = ["rccl"]
+            name = min(ok, key=lambda n: rec["ms"][n]) if ok else "rccl"
+        else:
+            comm = gg.comm
+            if not comm.one_node:
+                rec["reason"] = "ranks on several nodes: IPC peer mappings need one node"
+                name = "rccl"
+            else:
+                shared = _shared_device(comm)
+                _halo.use_transport("staged")
+                R = [_probe(A, int(gg.me), int(gg.nprocs)) for A in fields]
+                _halo.update_halo_(*R)
+                torch.cuda.synchronize()
+                skip = {"rccl": "skipped: ranks share a GPU (RCCL refuses duplicate devices)"} if shared else None
+                rec["checked"], rec["ms"] = _check_and_time(fields, list(DEFAULT_CANDIDATES), _halo.use_transport,
+                                                            comm, int(gg.me), int(gg.nprocs), R, AUTO_STEPS, skip)
+                del R
+                ok = [n for n in DEFAULT_CANDIDATES if rec["checked"].get(n) == "ok"]
+                if ok:
+                    name = min(ok, key=lambda n: rec["ms"][n])
+                else:
+                    warnings.warn(f"update_halo_ (IGG_TRANSPORT=auto): no device transport passed the probe "
+                                  f"exchange ({rec['checked']}); using the host-staged transport")
+                    name = "staged"
+        _halo.use_transport(name)
+    rec["chosen"] = name
+    return name, rec

@@ -14,10 +14,14 @@ On MI355X device data always moves device-resident (RCCL), so the "aware" flags
 are informational; ``loopvectorization[d]`` selects the threaded host copy for
 CPU fields in dim ``d`` (default: on).
 
-Framework knobs (new): ``IGG_TRANSPORT`` (``rccl`` | ``torch`` | ``staged``)
-for GPU point-to-point (``staged`` = host-staged gloo, the reference's
-non-GPU-aware path), ``IGG_STENCIL_VARIANT`` (int or ``auto``), ``IGG_DEBUG_SYNC``
-(synchronise after every halo update), ``IGG_QUIET``.
+Framework knobs (new): ``IGG_TRANSPORT`` (``auto`` | ``put`` | ``rccl`` |
+``torch`` | ``staged``) for GPU point-to-point: ``auto`` (default) checks
+``put`` and ``rccl`` bitwise against the host-staged exchange on the first
+eager device exchange of each field set and keeps the faster (``rccl`` across
+nodes; parallel/transport_select.py); ``put`` = one-sided IPC stores over xGMI
+(one node); ``rccl`` = grouped ncclSend/ncclRecv; ``staged`` = host-staged
+gloo, the reference's non-GPU-aware path. Also ``IGG_STENCIL_VARIANT`` (int or
+``auto``), ``IGG_DEBUG_SYNC`` (synchronise after every halo update), ``IGG_QUIET``.
 """
 from __future__ import annotations
 
@@ -59,9 +63,9 @@ def parse_loopvectorization(env: Mapping[str, str] | None = None) -> list[bool]:
 
 def transport_choice(env: Mapping[str, str] | None = None) -> str:
     env = os.environ if env is None else env
-    t = env.get("IGG_TRANSPORT", "rccl").strip().lower()
-    if t not in ("rccl", "torch", "staged", "put"):
-        raise ValueError(f"IGG_TRANSPORT must be 'rccl', 'torch', 'staged' or 'put' (got {t!r})")
+    t = env.get("IGG_TRANSPORT", "auto").strip().lower()
+    if t not in ("auto", "rccl", "torch", "staged", "put"):
+        raise ValueError(f"IGG_TRANSPORT must be 'auto', 'put', 'rccl', 'torch' or 'staged' (got {t!r})")
     return t
 
 

@@ -5,7 +5,8 @@
 # usage: scripts/gpu_run.sh TAG STEP [STEP ...]
 #   Every STEP is one quoted argument: "[VAR=value ...] KIND[@SECONDS] [ARGS...]"
 #   KIND  smoke                      __graft_entry__.smoke()
-#         pytest  [pytest args]      python -u -m pytest -x -q --timeout 120 (-m gpu unless -m given)
+#         pytest  [pytest args]      python -u -m pytest -x -q --timeout 120 (-m gpu unless -m given;
+#                                    --kor=a,b,c for -k "a or b or c")
 #         bench   [bench.py args]    python bench.py ... (prints the JSON summary line)
 #         py      script.py [args]   any python script of the repo
 #         prof    [bench.py args]    rocprofv3 --kernel-trace --stats around bench.py
@@ -36,7 +37,12 @@ for step in "$@"; do
     pytest)
       to=${to:-900}
       marks=(-m gpu); for a in "${args[@]}"; do [[ $a == -m ]] && marks=(); done
-      cmd=(python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider "${marks[@]}" "${args[@]}") ;;
+      # --kor=a,b,c -> -k "a or b or c" (a step is split on whitespace)
+      pargs=()
+      for a in "${args[@]}"; do
+        if [[ $a == --kor=* ]]; then k=${a#--kor=}; pargs+=(-k "${k//,/ or }"); else pargs+=("$a"); fi
+      done
+      cmd=(python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider "${marks[@]}" "${pargs[@]}") ;;
     bench) to=${to:-400}; cmd=(python -u bench.py "${args[@]}") ;;
     py) to=${to:-400}; cmd=(python -u "${args[@]}") ;;
     prof)

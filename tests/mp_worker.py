@@ -425,6 +425,92 @@ def scenario_select_transport(dev):
     print(f"rank {me} select transport OK", flush=True)
 
 
+def scenario_auto_transport(dev, expect):
+    """IGG_TRANSPORT=auto (the default): the first eager device exchange of a
+    field set checks put and rccl against the host-staged exchange and keeps
+    the fastest that passed, per field-set signature. ``expect``: the
+    transport it must choose ('put' on ranks sharing a GPU, where RCCL is
+    skipped; 'staged' when put's peer mapping is injected to fail there;
+    'fastest' with one rank per device). The caller's halo is exact either way."""
+    from igg.parallel import halo as H
+
+    device = _device(dev)
+    n = 20
+    me, dims, nprocs, coords, comm = igg.init_global_grid(n, n - 2, 12, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    gg = igg.get_global_grid()
+    assert H.auto_transport() and H.transport_name() == "auto", H.transport_name()
+    for dt in (torch.float64, torch.float32):
+        A = torch.zeros(n, n - 2, 12, dtype=dt)
+        encode(A)
+        ref = expected_after_halo(A, has_halo(A, gg), gg.neighbors.tolist())
+        X = zero_boundaries(A.clone()).to(device)
+        igg.update_halo_(X)
+        igg.update_halo_(X)  # the cached choice, no second selection
+        bad = (X.cpu() != ref).nonzero()
+        assert bad.shape[0] == 0, f"rank {me}: halo mismatch ({dt}) at {bad[:6].tolist()}"
+    log = H.tuned_transports()
+    print(f"rank {me} auto transport {log}", flush=True)
+    assert len(log) == 2, log  # one selection per signature (two dtypes)
+    for rec in log:
+        if expect == "fastest":
+            assert rec["checked"] == {"put": "ok", "rccl": "ok"}, rec
+            assert rec["chosen"] == min(rec["ms"], key=rec["ms"].get), rec
+        else:
+            assert rec["chosen"] == expect, rec
+            assert rec["checked"]["rccl"].startswith("skipped"), rec
+            if expect == "staged":
+                assert "could not map" in rec["checked"]["put"], rec
+    assert H.transport_name() == {"staged": "gloo-staged"}.get(log[-1]["chosen"], log[-1]["chosen"])
+    assert H.auto_transport()
+    H.set_transport("staged")  # an explicit choice ends the automatic one
+    assert not H.auto_transport()
+    igg.finalize_global_grid()
+    print(f"rank {me} auto transport OK", flush=True)
+
+
+def scenario_coherence(dev, form, nbytes, rounds):
+    """docs/COHERENCE.md fact 4 with WARM caches (igg/coherence.hpp): rank 0
+    reads its receive arena from 2 workgroups per CU (every XCD's L2 holds
+    every line), rank 1 stores a new value into it with the production
+    system-scope stores and publishes it with the production synchronisation
+    (``form``: 'kernel' = put_sync_kernel on both sides, 'inkernel' =
+    step_sync_exit_wg / step_sync_enter_wg inside the kernels); rank 0 then
+    reads every word from every XCD. Any stale line is a mismatch."""
+    device = _device(dev)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 8, 8, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    assert nprocs == 2
+    gg = igg.get_global_grid()
+    mesh = igg.native.PeerMesh(gg.comm.rank, gg.comm.size, gg.comm._allgather_bytes)
+    probe = igg.native.CoherenceProbe(mesh, int(nbytes))
+    ik = form == "inkernel"
+    s = torch.cuda.current_stream(device).cuda_stream
+    bad = []
+    if me == 0 and ik:
+        bad.append(probe.check(0, True, s))  # the reader's step 1 consumes the writer's step 0
+    for e in range(1, int(rounds) + 1):
+        if me == 0:
+            probe.warm(s)  # every XCD's L2 now holds the arena's lines (value e - 1)
+            torch.cuda.synchronize()
+        comm.barrier()  # the writer starts only after the warm reads completed
+        if me == 1:
+            probe.write(e, ik, s)
+        else:
+            bad.append(probe.check(e, ik, s))
+    torch.cuda.synchronize()
+    comm.barrier()
+    mesh.check_error()  # no synchronisation timed out
+    if me == 0:
+        print(f"rank 0 coherence {form} {int(nbytes) >> 10} KiB x {rounds} rounds ({probe.workgroups} workgroups "
+              f"per read): stale reads {sum(bad)}, per round {bad[:8]}", flush=True)
+        assert sum(bad) == 0, f"stale reads after the synchronisation: {bad}"
+    del probe
+    mesh.close()
+    igg.finalize_global_grid()
+    print(f"rank {me} coherence OK", flush=True)
+
+
 def scenario_put_regrow():
     """Put transport with field sets that force the receive arenas to grow
     (a collective re-export of IPC memory) several times (growth floor

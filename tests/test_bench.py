@@ -138,6 +138,7 @@ def test_driver_torchrun_launch_form():
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(420)  # subprocess bound 280 s + import/launch headroom (pytest.ini: a timeout aborts the session)
 @pytest.mark.parametrize("inject", ["", "fused_post"])
 def test_share_gpu_post_timing_checks(inject):
     """Two ranks on one GPU (put transport, fused exchange): the JSON carries

@@ -188,6 +188,26 @@ def test_fused_loopback_graph_and_mode_switches(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 8, 64, 72, 16, 88])
+@pytest.mark.parametrize("n2", [320, 512])
+@pytest.mark.parametrize("periods", [(1, 1, 1), (1, 0, 1), (0, 0, 1)])
+def test_fused_dpp_z_matches_update_halo(gpu, mode, n2, periods):
+    """Fused variant 48 (tiling 9, z-edge lane moves as DPP row shifts,
+    ZDPP): n2 = 320 / 512 put the high edge's rows inside the edge lane's
+    16-lane row (zh = 15 / 63), so the DPP form runs; bitwise equal to
+    stencil + update_halo_ in every send form (incl. z unpack and the
+    in-kernel step sync)."""
+    a, b = _pair((20, 26, n2), periods, torch.float64, 48, mode=mode)
+    a.run(7)
+    b.run(7)
+    b.sync_halo()
+    torch.cuda.synchronize()
+    b.check()
+    assert torch.equal(a.T, b.T)
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("graph", [False, True])
 def test_fused_receive_form_switch_reprimes(gpu, graph):
     """Switching the send mode's receive form mid-run (arena z 8 -> z unpack
@@ -201,7 +221,9 @@ def test_fused_receive_form_switch_reprimes(gpu, graph):
     for mode in (72, 12, 88, 8):
         b.fused_mode = mode
         if graph:
-            b.capture(steps=2)
+            k0 = b._fstep
+            b.capture(steps=2)  # re-primes with one eager step of the new form
+            a.run(b._fstep - k0)
         a.run(5)
         b.run(5)
         b.sync_halo()

@@ -85,10 +85,11 @@ def test_onephase_one_sided_mispairs_and_is_refused_over_rccl():
         class _R:
             name = "rccl"
 
-        H._loopback_comm = _R()
+        H._loopback_comm = H._loopback_comms["rccl"] = _R()
         with pytest.raises(igg.IGGError, match="one-sided"):
             H.set_halo_mode("onephase")
     finally:
         H._loopback_one_sided = False
         H._loopback_comm = None
+        H._loopback_comms.clear()
         igg.finalize_global_grid(finalize_MPI=False)

@@ -222,6 +222,20 @@ def test_select_transport(dev):
     run_ranks(2, "select_transport", dev, timeout=150)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("inject,expect", [("", "put"), ("peer_map@1", "staged")])
+def test_auto_transport_shared_gpu(inject, expect):
+    """IGG_TRANSPORT=auto (default) on ranks sharing one GPU: the first
+    exchange per field set checks put against the host-staged exchange (RCCL
+    refuses shared devices: skipped) and keeps it; with put's peer mapping
+    failing on one rank, every rank falls back to the staged transport
+    together. Halos bitwise exact in both."""
+    env = {"IGG_TRANSPORT": "auto", "IGG_PUT_TIMEOUT": "20"}
+    if inject:
+        env["IGG_INJECT_FAIL"] = inject
+    run_ranks(2, "auto_transport", "gpu", expect, env_extra=env, timeout=150)
+
+
 # --- fused halo exchange (stencil kernel stores into the neighbours' arenas)
 SLOW = pytest.mark.slow  # redundant cases: IGG_TEST_SLOW=1 (conftest.py)
 

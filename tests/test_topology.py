@@ -67,6 +67,7 @@ def test_env_precedence():
     # loopvectorization: per-dim only honoured if the global one set all dims true
     assert config.parse_loopvectorization({"IGG_LOOPVECTORIZATION_DIMX": "1"}) == [False] * 3
     assert config.parse_loopvectorization({"IGG_LOOPVECTORIZATION": "1", "IGG_LOOPVECTORIZATION_DIMX": "0"}) == [False, True, True]
-    assert config.transport_choice({}) == "rccl"
+    assert config.transport_choice({}) == "auto"
+    assert config.transport_choice({"IGG_TRANSPORT": "PUT"}) == "put"
     with pytest.raises(ValueError):
         config.transport_choice({"IGG_TRANSPORT": "mpi"})

@@ -11,7 +11,7 @@ arch VGPRs compiles to), selects, scratch, vector memory and LDS. The x-march
 loop of each per-wave sweep form of the fused kernel is one of the large
 loops, so the per-form cost of the exchange can be read without a GPU.
 
-Usage: python tools/loop_census.py UNIT KERNEL_SUBSTRING [--min 300]
+Usage: python tools/loop_census.py UNIT|OBJECT.o KERNEL_SUBSTRING [--min 300] [--all]
   e.g. python tools/loop_census.py fused_t9_f64 'ELb0ELi2359503E'
 """
 from __future__ import annotations
@@ -50,7 +50,8 @@ TARGET = re.compile(r"<[^>]*\+0x([0-9a-f]+)>")
 
 
 def disassemble(unit: str) -> str:
-    obj = kr.BUILD / f"{unit}.hip.opt-fpc0.o"
+    """``unit``: a unit of build/native, or the path of any HIP object."""
+    obj = Path(unit) if unit.endswith(".o") else kr.BUILD / f"{unit}.hip.opt-fpc0.o"
     with tempfile.TemporaryDirectory() as td:
         co = kr._code_object(obj, Path(td))
         return subprocess.run([str(kr.LLVM / "llvm-objdump"), "-d", f"--mcpu={kr.ARCH}", str(co)],
@@ -110,20 +111,22 @@ def main() -> int:
     ap.add_argument("unit")
     ap.add_argument("kernel", help="substring of the (mangled) kernel symbol")
     ap.add_argument("--min", type=int, default=300, help="smallest loop (instructions) to report")
+    ap.add_argument("--all", action="store_true", help="every kernel matching the substring")
     a = ap.parse_args()
     fns = functions(disassemble(a.unit))
     hits = [k for k in fns if a.kernel in k]
-    if len(hits) != 1:
+    if not hits or (len(hits) > 1 and not a.all):
         print(f"{len(hits)} kernels match {a.kernel!r}: {hits[:4]}", file=sys.stderr)
         return 1
-    ins = fns[hits[0]]
     cols = ["total"] + [n for n, _ in CLASSES]
-    print(f"{hits[0]}: {len(ins)} instructions")
-    print("| loop | " + " | ".join(cols) + " |")
-    print("|---" * (len(cols) + 1) + "|")
-    for j, i in loops(ins, a.min):
-        c = census(ins[j:i + 1])
-        print(f"| {ins[j][0]:x}-{ins[i][0]:x} | " + " | ".join(str(c[k]) for k in cols) + " |")
+    for h in hits:
+        ins = fns[h]
+        print(f"{h}: {len(ins)} instructions")
+        print("| loop | " + " | ".join(cols) + " |")
+        print("|---" * (len(cols) + 1) + "|")
+        for j, i in loops(ins, a.min):
+            c = census(ins[j:i + 1])
+            print(f"| {ins[j][0]:x}-{ins[i][0]:x} | " + " | ".join(str(c[k]) for k in cols) + " |")
     return 0
 
 
