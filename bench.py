@@ -65,7 +65,10 @@ import time
 # deferred-send mode is kept in the A/B for real xGMI links, where a remote
 # store's acknowledgement is slower than in the loopback measurements.
 FUSED_CANDIDATES = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (0, 1, 1), (9, 0, 2), (9, 0, 3), (14, 0, 3),
-                    (40, 0, 2), (42, 0, 2), (42, 1, 2), (50, 0, 2), (50, 1, 2), (50, 1, 3))
+                    (40, 0, 2), (42, 0, 2), (42, 1, 2), (50, 0, 2), (50, 1, 2), (50, 1, 3),
+                    # round 6: tiling 9 with DPP z-edge lane moves (ties v9 at a loopback corner,
+                    # profiles/r6_corner/NOTES.md; a real node's A/B decides)
+                    (48, 0, 3), (48, 8, 2))
 # Direct z (send mode bit 4: the z faces go straight into the neighbours' next
 # T, no z receive code in the z-edge waves; igg/fused.hpp). Only with a z
 # neighbour (without one these equal their mode & 3 forms).
@@ -318,7 +321,11 @@ def _all_ranks(comm, v: float) -> list:
 # local first, odd pairs step first: a fixed order biased round 5's N=1 value
 # to 1.005 with a cold first local sample), after one untimed run of each form;
 # medians.
-EFF_PAIRS = 5
+EFF_PAIRS = 7
+# steps per efficiency sample: at least this many (a 20-step sample of a
+# 0.6 ms step is 12 ms, and its +-0.3 % run-to-run noise moved the N=1 value
+# by 0.0045 on a round-6 box)
+EFF_MIN_STEPS = 100
 LOCAL_GRAPH_STEPS = 10
 
 
@@ -370,6 +377,7 @@ def measure_efficiency(model, comm, log, graph: bool, k: int, pairs: int = EFF_P
     if not hasattr(model, "local_step"):
         return None
     saved = _begin_local_steps(model)
+    k = max(EFF_MIN_STEPS, k)
     k = max(2, k + (k % 2))  # even: the ping-pong buffers keep their roles
     on_gpu = getattr(model, "device", None) is not None and model.device.type == "cuda"
     gl = None

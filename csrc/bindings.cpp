@@ -450,14 +450,28 @@ PYBIND11_MODULE(_igg_native, m) {
       .def(py::init<std::shared_ptr<PeerMesh>, size_t>(), py::arg("mesh"), py::arg("bytes"),
            "Collective over a 2-rank mesh (reader 0, writer 1): arenas of `bytes` (igg/coherence.hpp).")
       .def("warm", [](CoherenceProbe& p, uintptr_t s) { p.warm(as_stream(s)); }, py::arg("stream"))
-      .def("write", [](CoherenceProbe& p, uint64_t v, bool in_kernel, uintptr_t s) { p.write(v, in_kernel, as_stream(s)); },
-           py::arg("value"), py::arg("in_kernel"), py::arg("stream"))
+      .def("write",
+           [](CoherenceProbe& p, uint64_t v, bool in_kernel, uintptr_t s, bool plain) {
+             p.write(v, in_kernel, as_stream(s), plain);
+           },
+           py::arg("value"), py::arg("in_kernel"), py::arg("stream"), py::arg("plain") = false)
       .def("check",
            [](CoherenceProbe& p, uint64_t v, bool in_kernel, uintptr_t s) {
              py::gil_scoped_release nogil;
              return p.check(v, in_kernel, as_stream(s));
            },
            py::arg("value"), py::arg("in_kernel"), py::arg("stream"))
+      .def("control",
+           [](CoherenceProbe& p, uint64_t v, uint64_t target, bool l2, uintptr_t s) {
+             p.control(v, target, l2, as_stream(s));
+           },
+           py::arg("value"), py::arg("target"), py::arg("l2"), py::arg("stream"))
+      .def("mismatches",
+           [](CoherenceProbe& p, uintptr_t s) {
+             py::gil_scoped_release nogil;
+             return p.mismatches(as_stream(s));
+           },
+           py::arg("stream"))
       .def_property_readonly("workgroups", &CoherenceProbe::workgroups)
       .def_property_readonly("words", &CoherenceProbe::words);
   py::class_<PutTransport, Transport, std::shared_ptr<PutTransport>>(m, "PutTransport")

@@ -38,13 +38,19 @@ class CoherenceProbe {
   void warm(hipStream_t s);
   // W: stores `value` into every word of R's arena (st_sys), then publishes:
   // in_kernel false -> put_sync_kernel, true -> step_sync_exit_wg in the kernel.
-  void write(uint64_t value, bool in_kernel, hipStream_t s);
+  // plain: write-back stores instead (positive control of the test's sensitivity).
+  void write(uint64_t value, bool in_kernel, hipStream_t s, bool plain = false);
   // R: synchronises with W (put_sync_kernel, or step_sync_enter_wg in every
   // workgroup of the check kernel), then every workgroup compares every word
   // with `value`; returns the number of mismatching reads (stream-synchronous).
   // In-kernel form: R's step c+1 consumes W's step c, so R's first check
   // (value 0, the zero-filled arena) precedes W's first write.
   int64_t check(uint64_t value, bool in_kernel, hipStream_t s);
+  // R, negative control: launches (asynchronously) a kernel that warms the
+  // caches, waits for ARRIVED[W] >= target with relaxed polls and NO acquire,
+  // then re-reads (l2: skipping the L1); mismatches() returns its count.
+  void control(uint64_t value, uint64_t target, bool l2, hipStream_t s);
+  int64_t mismatches(hipStream_t s);
   int workgroups() const { return wgs_; }
   size_t words() const { return words_; }
 

@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(BLOCK) coh_read_kernel(const uint64_t* __restr
 // acknowledgement means the bytes left for R's memory), then either nothing
 // (a put_sync_kernel publishes next on the stream) or the in-kernel exit.
 __global__ void __launch_bounds__(BLOCK) coh_write_kernel(uint64_t* a, int64_t n, uint64_t value, StepSync s,
-                                                         int in_kernel) {
+                                                         int in_kernel, int plain) {
   __shared__ uint64_t wsync[4];
   const int lane = threadIdx.x & 63;
   uint64_t c = 0;
@@ -59,9 +59,46 @@ __global__ void __launch_bounds__(BLOCK) coh_write_kernel(uint64_t* a, int64_t n
     c = step_sync_enter_wg(s, lane, wsync);
   }
   const int64_t stride = static_cast<int64_t>(gridDim.x) * BLOCK;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < n; i += stride) st_sys(a + i, value);
+  // plain (positive control only): write-back stores, which may stay dirty in
+  // this XCD's L2 - the writer-side hazard the production st_sys avoids
+  if (plain) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < n; i += stride) a[i] = value;
+  } else {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < n; i += stride) st_sys(a + i, value);
+  }
   __builtin_amdgcn_s_waitcnt(0);
   if (in_kernel) step_sync_exit_wg(s, lane, c, wsync, WAVES);
+}
+
+// Negative control (no acquire): every workgroup reads the arena (warm),
+// waits until W's ARRIVED reaches `target` with relaxed polls only (no fence,
+// no kernel boundary), then reads every word again - plain loads (which may
+// hit this CU's L1 and the XCD's L2) or, `l2`, loads that skip the L1 (sc0),
+// which can hit only the L2 - and counts the words still != value. A nonzero
+// count shows that the caches DO hold stale lines, i.e. that the production
+// forms' zero comes from their synchronisation, not from an uncached arena.
+__global__ void __launch_bounds__(BLOCK) coh_control_kernel(const uint64_t* __restrict__ a, int64_t n, uint64_t value,
+                                                           unsigned long long* bad, uint64_t* sink,
+                                                           const uint64_t* arrived, uint64_t target,
+                                                           uint64_t* my_flags, int64_t timeout, int l2) {
+  uint64_t acc = 0;
+  for (int64_t i = threadIdx.x; i < n; i += BLOCK) acc ^= a[i];
+  sink[static_cast<int64_t>(blockIdx.x) * BLOCK + threadIdx.x] = acc;
+  if (threadIdx.x == 0) spin_geq(arrived, target, my_flags, timeout, 0x500);
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(a), static_cast<short>(0), 0x7fffffff, 0x00020000);
+  unsigned long long nbad = 0;
+  for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
+    uint64_t v;
+    if (l2) {
+      v = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rs, static_cast<int>(i * 8), 0, 1));
+    } else {
+      v = a[i];
+    }
+    nbad += v != value;
+  }
+  if (nbad) atomicAdd(bad, nbad);
 }
 
 StepSync probe_sync(const PeerMesh& m, int64_t units) {
@@ -124,14 +161,31 @@ void CoherenceProbe::warm(hipStream_t s) {
   IGG_HIP_CHECK(hipGetLastError());
 }
 
-void CoherenceProbe::write(uint64_t value, bool in_kernel, hipStream_t s) {
+void CoherenceProbe::write(uint64_t value, bool in_kernel, hipStream_t s, bool plain) {
   if (mesh_->rank() != 1) fail("CoherenceProbe.write: the writer is rank 1");
   const int wg = wgs_ / 2;  // every workgroup resident (the exit counts them all)
   hipLaunchKernelGGL(coh_write_kernel, dim3(wg), dim3(BLOCK), 0, s, reinterpret_cast<uint64_t*>(mesh_->arena(0)),
                      static_cast<int64_t>(words_), value, in_kernel ? probe_sync(*mesh_, wg) : StepSync{},
-                     in_kernel ? 1 : 0);
+                     in_kernel ? 1 : 0, plain ? 1 : 0);
   IGG_HIP_CHECK(hipGetLastError());
   if (!in_kernel) launch_put_sync(probe_put_sync(*mesh_), s);
+}
+
+void CoherenceProbe::control(uint64_t value, uint64_t target, bool l2, hipStream_t s) {
+  if (mesh_->rank() != 0) fail("CoherenceProbe.control: the reader is rank 0");
+  IGG_HIP_CHECK(hipMemsetAsync(bad_, 0, sizeof(unsigned long long), s));
+  uint64_t* f = mesh_->flags(0);
+  hipLaunchKernelGGL(coh_control_kernel, dim3(wgs_), dim3(BLOCK), 0, s,
+                     reinterpret_cast<const uint64_t*>(mesh_->arena(0)), static_cast<int64_t>(words_), value, bad_,
+                     sink_, f + PutFlags::ARRIVED + 1, target, f, mesh_->timeout_ticks(), l2 ? 1 : 0);
+  IGG_HIP_CHECK(hipGetLastError());
+}
+
+int64_t CoherenceProbe::mismatches(hipStream_t s) {
+  unsigned long long h = 0;
+  IGG_HIP_CHECK(hipMemcpyAsync(&h, bad_, sizeof(h), hipMemcpyDeviceToHost, s));
+  IGG_HIP_CHECK(hipStreamSynchronize(s));
+  return static_cast<int64_t>(h);
 }
 
 int64_t CoherenceProbe::check(uint64_t value, bool in_kernel, hipStream_t s) {

@@ -469,7 +469,7 @@ def scenario_auto_transport(dev, expect):
     print(f"rank {me} auto transport OK", flush=True)
 
 
-def scenario_coherence(dev, form, nbytes, rounds):
+def scenario_coherence(dev, form, nbytes, rounds, plain_writer=0):
     """docs/COHERENCE.md fact 4 with WARM caches (igg/coherence.hpp): rank 0
     reads its receive arena from 2 workgroups per CU (every XCD's L2 holds
     every line), rank 1 stores a new value into it with the production
@@ -495,20 +495,62 @@ def scenario_coherence(dev, form, nbytes, rounds):
             torch.cuda.synchronize()
         comm.barrier()  # the writer starts only after the warm reads completed
         if me == 1:
-            probe.write(e, ik, s)
+            probe.write(e, ik, s, bool(int(plain_writer)))
         else:
             bad.append(probe.check(e, ik, s))
     torch.cuda.synchronize()
     comm.barrier()
     mesh.check_error()  # no synchronisation timed out
     if me == 0:
-        print(f"rank 0 coherence {form} {int(nbytes) >> 10} KiB x {rounds} rounds ({probe.workgroups} workgroups "
-              f"per read): stale reads {sum(bad)}, per round {bad[:8]}", flush=True)
-        assert sum(bad) == 0, f"stale reads after the synchronisation: {bad}"
+        print(f"rank 0 coherence {form}{' PLAIN-STORE WRITER' if int(plain_writer) else ''} "
+              f"{int(nbytes) >> 10} KiB x {rounds} rounds ({probe.workgroups} workgroups per read): "
+              f"stale reads {sum(bad)}, per round {bad[:8]}", flush=True)
+        if not int(plain_writer):
+            assert sum(bad) == 0, f"stale reads after the synchronisation: {bad}"
     del probe
     mesh.close()
     igg.finalize_global_grid()
     print(f"rank {me} coherence OK", flush=True)
+
+
+def scenario_coherence_control(dev, nbytes, rounds, l2):
+    """Negative control of scenario_coherence: the reader warms its caches
+    and then re-reads the arena in the SAME kernel after seeing the writer's
+    ARRIVED flag with relaxed polls only - no acquire, no kernel boundary
+    (l2 = 1: the re-read skips the L1). Prints the stale-read count; a
+    nonzero count shows that the warm caches do hold stale lines, so the
+    production forms' zero (scenario_coherence) comes from their acquires."""
+    import time
+
+    device = _device(dev)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 8, 8, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    gg = igg.get_global_grid()
+    mesh = igg.native.PeerMesh(gg.comm.rank, gg.comm.size, gg.comm._allgather_bytes)
+    probe = igg.native.CoherenceProbe(mesh, int(nbytes))
+    s = torch.cuda.current_stream(device).cuda_stream
+    bad = []
+    for e in range(1, int(rounds) + 1):
+        if me == 0:
+            probe.control(e, e, bool(int(l2)), s)
+            time.sleep(0.005)  # the kernel's warm read completes before the writer starts
+        comm.barrier()
+        if me == 1:
+            probe.write(e, False, s)
+            torch.cuda.synchronize()
+        else:
+            bad.append(probe.mismatches(s))
+    torch.cuda.synchronize()
+    comm.barrier()
+    mesh.check_error()
+    if me == 0:
+        print(f"rank 0 coherence control ({'L1 bypass' if int(l2) else 'plain loads'}, no acquire) "
+              f"{int(nbytes) >> 10} KiB x {rounds} rounds: stale reads {sum(bad)} of "
+              f"{int(rounds) * probe.words * probe.workgroups}, per round {bad[:8]}", flush=True)
+    del probe
+    mesh.close()
+    igg.finalize_global_grid()
+    print(f"rank {me} coherence control done", flush=True)
 
 
 def scenario_put_regrow():

@@ -259,7 +259,7 @@ def test_efficiency_phase_leaves_a_consistent_state(model):
         m.run(3)
         before = {n: getattr(m, n).clone() for n in b._state(m)}
         e = b.measure_efficiency(m, _C(), lambda s: None, False, 4)
-        assert e is not None and e["steps"] == 4
+        assert e is not None and e["steps"] == b.EFF_MIN_STEPS
         if model == "acoustic":
             assert all(torch.equal(before[n], getattr(m, n)) for n in before)
             assert m._entry

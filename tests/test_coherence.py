@@ -26,3 +26,31 @@ def test_warm_cache_coherence_shared_gpu(form, nbytes, rounds):
     outs = run_ranks(2, "coherence", "gpu", form, nbytes, rounds,
                      env_extra={"IGG_PUT_TIMEOUT": "20"}, timeout=150)
     assert any("stale reads 0" in o for o in outs), outs[0][-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("l2", [0, 1])
+def test_warm_cache_control_without_acquire(l2):
+    """The same warm reader re-reading inside one kernel after a relaxed flag
+    poll, with no acquire (l2: skipping the L1): records how many stale words
+    the caches return without the production synchronisation (the test's
+    sensitivity; profiles/r6_coherence/NOTES.md). Only the run is asserted:
+    the count is hardware behaviour, not a property of this code."""
+    outs = run_ranks(2, "coherence_control", "gpu", 16 << 10, 20, l2, env_extra={"IGG_PUT_TIMEOUT": "20"},
+                     timeout=150)
+    line = [ln for ln in outs[0].splitlines() if "coherence control" in ln and "stale reads" in ln]
+    assert line, outs[0][-2000:]
+    print(line[0])
+
+
+@pytest.mark.gpu
+def test_plain_store_writer_control():
+    """Positive control: a writer with plain (write-back) stores instead of
+    st_sys, same synchronisation. Records how many stale words the reader
+    then gets (profiles/r6_coherence/NOTES.md) - the writer-side hazard that
+    the production system-scope stores exist for."""
+    outs = run_ranks(2, "coherence", "gpu", "kernel", 4 << 20, 20, 1, env_extra={"IGG_PUT_TIMEOUT": "20"},
+                     timeout=150)
+    line = [ln for ln in outs[0].splitlines() if "PLAIN-STORE WRITER" in ln]
+    assert line, outs[0][-2000:]
+    print(line[0])
