@@ -27,6 +27,7 @@
 #include "igg/stencil.hpp"
 #include "igg/topology.hpp"
 #include "igg/trace.hpp"
+#include "igg/vmm.hpp"
 
 namespace igg {
 void launch_zcol_probe(int dir, const void* src, void* dst, int64_t rows, int64_t pitch, int aux,
@@ -92,7 +93,8 @@ void flush_deferred_frees() {
       (void)hipDeviceSynchronize();  // no kernel may still use the buffers
       synced = dev;
     }
-    (void)hipFree(p);
+    if (vmm_find(p, nullptr, nullptr)) vmm_free(p);  // a MemKind::Vmm field
+    else (void)hipFree(p);
   }
   (void)hipSetDevice(cur);
 }
@@ -446,6 +448,37 @@ PYBIND11_MODULE(_igg_native, m) {
       .def("check_error", &PeerMesh::check_error)
       .def("clear_error", &PeerMesh::clear_error)
       .def("close", &PeerMesh::close);
+  // --- HIP virtual memory management (allocations >= 2 GiB across processes)
+  m.def("vmm_granularity", &vmm_granularity, py::arg("device"));
+  m.def("vmm_alloc",
+        [](size_t bytes) {
+          size_t mapped = 0;
+          void* p = vmm_alloc(bytes, &mapped);
+          return py::make_tuple(reinterpret_cast<uintptr_t>(p), mapped);
+        },
+        py::arg("bytes"), "(pointer, mapped bytes) of new hipMemCreate memory on the current device");
+  m.def("vmm_export_fd", [](uintptr_t p) { return vmm_export_fd(reinterpret_cast<void*>(p)); }, py::arg("ptr"));
+  m.def("vmm_import_fd",
+        [](int fd, size_t size, double seconds) {
+          py::gil_scoped_release nogil;
+          return reinterpret_cast<uintptr_t>(vmm_import_fd(fd, size, seconds));
+        },
+        py::arg("fd"), py::arg("size"), py::arg("seconds"));
+  m.def("vmm_free", [](uintptr_t p) { vmm_free(reinterpret_cast<void*>(p)); }, py::arg("ptr"));
+  m.def("fd_listen", &fd_listen, py::arg("name"));
+  m.def("fd_serve",
+        [](int listener, int fd, int clients, double seconds) {
+          py::gil_scoped_release nogil;
+          fd_serve(listener, fd, clients, seconds);
+        },
+        py::arg("listener"), py::arg("fd"), py::arg("clients"), py::arg("seconds"));
+  m.def("fd_fetch",
+        [](const std::string& name, double seconds) {
+          py::gil_scoped_release nogil;
+          return fd_fetch(name, seconds);
+        },
+        py::arg("name"), py::arg("seconds"));
+  m.def("fd_close", &fd_close, py::arg("fd"));
   py::class_<CoherenceProbe, std::shared_ptr<CoherenceProbe>>(m, "CoherenceProbe")
       .def(py::init<std::shared_ptr<PeerMesh>, size_t>(), py::arg("mesh"), py::arg("bytes"),
            "Collective over a 2-rank mesh (reader 0, writer 1): arenas of `bytes` (igg/coherence.hpp).")

@@ -3,6 +3,9 @@
 #include "igg/fault.hpp"
 #include "igg/trace.hpp"
 #include "igg/ipc.hpp"
+#include "igg/vmm.hpp"
+
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -97,18 +100,82 @@ uint32_t get_u32(const std::string& r, size_t at) {
 
 }  // namespace
 
+// IGG_GATHER_VMM=0: large snapshots go through IPC staging chunks (rounds
+// 3-5) instead of one VMM staging buffer.
+bool vmm_staging() {
+  static const bool on = [] {
+    const char* e = std::getenv("IGG_GATHER_VMM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 PullGatherer::PullGatherer(int rank, int nranks, AllGather allgather)
     : rank_(rank), nranks_(nranks), allgather_(std::move(allgather)) {
   peer_key_.assign(nranks, std::string());
   peer_ev_.assign(nranks, nullptr);
   mapped_.assign(nranks, {});
+  mapped_vmm_.assign(nranks, 0);
+}
+
+std::string PullGatherer::vmm_record(void* base, size_t size, uint64_t off) {
+  int k = 0;
+  while (k < static_cast<int>(vexp_.size()) && vexp_[k].base != base) ++k;
+  if (k == static_cast<int>(vexp_.size())) {
+    VmmExport e;
+    e.base = base;
+    e.fd = vmm_export_fd(base);
+    static int serial = 0;
+    e.name = "igg-gather-" + std::to_string(::getpid()) + "-" + std::to_string(rank_) + "-" + std::to_string(serial++);
+    e.listener = fd_listen(e.name);
+    vexp_.push_back(e);
+  }
+  cur_vexp_ = k;
+  std::string rec(1, 'V');
+  put_u32(rec, static_cast<uint32_t>(vexp_[k].name.size()));
+  rec += vexp_[k].name;
+  const uint64_t sz = size;
+  rec.append(reinterpret_cast<const char*>(&sz), 8);
+  rec.append(reinterpret_cast<const char*>(&off), 8);
+  return rec;
+}
+
+void PullGatherer::close_mapped(int p) {
+  auto& per = mapped_[p];
+  if (!per.empty()) {
+    for (hipStream_t q : side_) IGG_HIP_CHECK(hipStreamSynchronize(q));  // rare: old copies drained
+    for (auto& m : per) {
+      if (mapped_vmm_[p]) vmm_free(m.second);
+      else ipc_close(m.second);
+    }
+  }
+  per.clear();
+  mapped_vmm_[p] = 0;
+}
+
+void PullGatherer::free_vmm() {
+  for (auto& e : vexp_) {
+    fd_close(e.listener);
+    fd_close(e.fd);
+  }
+  vexp_.clear();
+  cur_vexp_ = -1;
+  if (vstage_) vmm_free(vstage_);
+  for (void* v : vretired_) vmm_free(v);
+  vstage_ = nullptr;
+  vstage_bytes_ = 0;
+  vretired_.clear();
 }
 
 PullGatherer::~PullGatherer() {
   for (hipStream_t s : side_) (void)hipStreamSynchronize(s);
-  for (auto& per : mapped_)
-    for (auto& m : per)
-      if (m.second) (void)hipIpcCloseMemHandle(m.second);
+  for (int p = 0; p < static_cast<int>(mapped_.size()); ++p)
+    for (auto& m : mapped_[p])
+      if (m.second) {
+        if (mapped_vmm_[p]) vmm_free(m.second);
+        else (void)hipIpcCloseMemHandle(m.second);
+      }
+  free_vmm();
   if (!stage_.empty() || !retired_.empty()) (void)hipDeviceSynchronize();
   for (char* c : stage_) (void)hipFree(c);
   for (char* c : retired_) (void)hipFree(c);
@@ -137,11 +204,16 @@ void PullGatherer::ensure_streams() {
 void PullGatherer::free() {
   if (pending_) fail("gather_async: free while a gather is pending (call wait() first)");
   for (hipStream_t s : side_) IGG_HIP_CHECK(hipStreamSynchronize(s));
-  for (auto& per : mapped_) {
-    for (auto& m : per)
-      if (m.second) (void)hipIpcCloseMemHandle(m.second);
-    per.clear();
+  for (int p = 0; p < static_cast<int>(mapped_.size()); ++p) {
+    for (auto& m : mapped_[p])
+      if (m.second) {
+        if (mapped_vmm_[p]) vmm_free(m.second);
+        else (void)hipIpcCloseMemHandle(m.second);
+      }
+    mapped_[p].clear();
+    mapped_vmm_[p] = 0;
   }
+  free_vmm();
   if (!stage_.empty() || !retired_.empty()) IGG_HIP_CHECK(hipDeviceSynchronize());
   for (char* c : stage_) IGG_HIP_CHECK(hipFree(c));
   for (char* c : retired_) IGG_HIP_CHECK(hipFree(c));
@@ -169,15 +241,33 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
   try {
     inject_fail("gather_export");
     std::string rec;  // after the event handle: 'D' handle offset | 'C' nchunks planes/chunk handles...
+    cur_vexp_ = -1;
     if (rank_ != root) {
       void* base = nullptr;
       size_t size = 0;
-      IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(a.ptr)));
+      bool vown = false;
+      const bool a_vmm = vmm_find(reinterpret_cast<const void*>(a.ptr), &base, &size, &vown) && vown;
+      if (!a_vmm) IGG_HIP_CHECK(hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(a.ptr)));
       bool forced = false;
       const size_t cap = chunk_cap(&forced);
+      const size_t abytes = plane * static_cast<size_t>(a.size[0]);
       // snapshot: `a` may change as soon as start() returns, so it is copied
       // into the staging chunks in any case (the chunks are the snapshot).
-      if (snapshot || size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
+      if (a_vmm && !snapshot) {
+        // a VMM allocation: exportable at any size, pulled in place
+        rec = vmm_record(base, size, a.ptr - reinterpret_cast<uintptr_t>(base));
+      } else if ((snapshot || size >= IPC_MAX_BYTES) && !forced && vmm_staging() && abytes >= IPC_MAX_BYTES / 2) {
+        // a large snapshot / an unexportable allocation: ONE VMM staging
+        // buffer (grow-only; a grown-out one is retired, its export name dies
+        // with it, so the root re-imports)
+        if (vstage_bytes_ < abytes) {
+          if (vstage_) vretired_.push_back(vstage_);
+          vstage_ = vmm_alloc(abytes, &vstage_bytes_);
+        }
+        IGG_HIP_CHECK(hipMemcpyAsync(vstage_, reinterpret_cast<const void*>(a.ptr), abytes, hipMemcpyDeviceToDevice,
+                                     stream));
+        rec = vmm_record(vstage_, vstage_bytes_, 0);
+      } else if (snapshot || size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
         // Stage into exportable chunks of whole planes (class comment).
         const int64_t ppc = std::max<int64_t>(1, static_cast<int64_t>(cap / std::max<size_t>(plane, 1)));
         const size_t cb = static_cast<size_t>(ppc) * plane;
@@ -244,6 +334,28 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
   for (auto& x : all) x.erase(0, 1);
   const int nside = static_cast<int>(side_.size());
   used_ = std::min(nranks_, nside);
+  // VMM records: the root asks every rank whose export it has not mapped yet
+  // for the file descriptor (one more host rendezvous, only when some rank
+  // published a 'V' record - every rank sees every record, so all agree).
+  auto vname = [&](const std::string& rec) {
+    const uint32_t n = rec.size() >= EH + 5 ? get_u32(rec, EH + 1) : 0;
+    return rec.size() >= EH + 5 + n + 16 ? rec.substr(EH + 5, n) : std::string();
+  };
+  bool any_v = false;
+  for (int p = 0; p < nranks_; ++p) any_v = any_v || (p != root && all[p].size() > EH && all[p][EH] == 'V');
+  std::string need;
+  if (any_v) {
+    std::string mine_need;
+    if (rank_ == root) {
+      mine_need.assign(nranks_, '0');
+      for (int p = 0; p < nranks_; ++p)
+        if (p != root && all[p].size() > EH && all[p][EH] == 'V' &&
+            !(mapped_vmm_[p] && mapped_[p].size() == 1 && mapped_[p][0].first == vname(all[p])))
+          mine_need[p] = '1';
+    }
+    const std::vector<std::string> needs = allgather_(mine_need);
+    need = needs[root];
+  }
   // The root maps the blocks and enqueues the pulls; a second status round
   // tells the peers whether that worked (they would otherwise wait for a
   // gather that never comes in wait()'s rendezvous).
@@ -272,6 +384,32 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
           }
           IGG_HIP_CHECK(hipStreamWaitEvent(s, peer_ev_[p], 0));
           const char mode = rec[EH];
+          if (mode == 'V') {
+            const std::string name = vname(rec);
+            if (name.empty()) fail("gather_async: malformed VMM record from rank ", p);
+            const size_t n = name.size();
+            uint64_t vsz = 0, off = 0;
+            std::memcpy(&vsz, rec.data() + EH + 5 + n, 8);
+            std::memcpy(&off, rec.data() + EH + 13 + n, 8);
+            if (need.size() == static_cast<size_t>(nranks_) && need[p] == '1') {
+              close_mapped(p);
+              inject_fail("gather_open");
+              const int fd = fd_fetch(name, first_contact_timeout());
+              void* q = nullptr;
+              try {
+                q = vmm_import_fd(fd, vsz, first_contact_timeout());
+              } catch (...) {
+                fd_close(fd);
+                throw;
+              }
+              fd_close(fd);
+              mapped_[p].emplace_back(name, q);
+              mapped_vmm_[p] = 1;
+            }
+            copy_block(static_cast<const char*>(mapped_[p][0].second) + off, dst, a.size, dims, c, 0, a.size[0],
+                       a.elem_bytes, s);
+            continue;
+          }
           const size_t nbuf = mode == 'C' && rec.size() >= EH + 9 ? get_u32(rec, EH + 1) : 1;
           const size_t hdr = mode == 'C' ? EH + 9 : EH + 1;
           if ((mode != 'C' && mode != 'D') || (mode == 'D' && rec.size() != hdr + MH + 8) ||
@@ -280,12 +418,8 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
           auto& per = mapped_[p];
           bool changed = per.size() != nbuf;
           for (size_t k = 0; k < nbuf && !changed; ++k) changed = per[k].first != rec.substr(hdr + k * MH, MH);
-          if (changed) {  // this rank's array (or staging) lives in other allocations now
-            if (!per.empty()) {
-              for (hipStream_t q : side_) IGG_HIP_CHECK(hipStreamSynchronize(q));  // rare: old copies drained
-              for (auto& m : per) ipc_close(m.second);
-            }
-            per.clear();
+          if (changed || mapped_vmm_[p]) {  // this rank's array (or staging) lives in other allocations now
+            close_mapped(p);
             inject_fail("gather_open");
             for (size_t k = 0; k < nbuf; ++k) {
               const std::string key = rec.substr(hdr + k * MH, MH);
@@ -311,6 +445,11 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
       }
       for (int k = 0; k < used_; ++k) IGG_HIP_CHECK(hipEventRecord(done_[k], side_[k]));
     } else {
+      // the root asked for this rank's VMM descriptor: hand it over (bounded)
+      if (need.size() == static_cast<size_t>(nranks_) && need[rank_] == '1') {
+        if (cur_vexp_ < 0) fail("gather_async: the root asked for a VMM export this rank did not publish");
+        fd_serve(vexp_[cur_vexp_].listener, vexp_[cur_vexp_].fd, 1, first_contact_timeout());
+      }
       const std::string& rec = all[root];
       if (rec.size() != EH * (1 + used_)) fail("gather_async: malformed handles from the root");
       if (static_cast<int>(root_done_.size()) < used_) {

@@ -108,6 +108,26 @@ class PullGatherer {
   std::vector<char*> stage_;  // own staging chunks (a large `a`), grow-only
   size_t stage_bytes_ = 0;    // bytes of each staging chunk
   std::vector<char*> retired_;  // grown-out staging chunks, freed at free() (never re-exported addresses)
+  // HIP VMM exports (vmm.hpp; round 6): an `a` living in a MemKind::Vmm
+  // allocation is published as-is at ANY size ('V' record: a socket name the
+  // root fetches the allocation's file descriptor from, once, plus size and
+  // offset), and a large snapshot is staged into ONE grow-only VMM buffer
+  // instead of IPC chunks. The root maps each once (cached by socket name)
+  // and pulls it as one block.
+  struct VmmExport {
+    void* base = nullptr;
+    int listener = -1, fd = -1;
+    std::string name;
+  };
+  std::vector<VmmExport> vexp_;
+  int cur_vexp_ = -1;           // the export published by the pending gather (non-root)
+  void* vstage_ = nullptr;      // VMM staging buffer (large snapshots)
+  size_t vstage_bytes_ = 0;
+  std::vector<void*> vretired_;
+  std::vector<char> mapped_vmm_;  // root: mapped_[p] holds VMM imports (vmm_free) rather than IPC maps
+  std::string vmm_record(void* base, size_t size, uint64_t off);
+  void close_mapped(int p);
+  void free_vmm();
   bool pending_ = false;
   int root_ = 0;
   int used_ = 0;  // copy streams used by the pending gather

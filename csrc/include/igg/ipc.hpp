@@ -23,6 +23,7 @@ enum class MemKind : int {
   FineGrained = 1, // hipDeviceMallocFinegrained
   Signal = 2,      // hipMallocSignalMemory
   Uncached = 3,    // hipDeviceMallocUncached (coherent across devices, bypasses L2)
+  Vmm = 4,         // hipMemCreate + map (vmm.hpp): exportable at any size (a file descriptor)
 };
 
 // Largest allocation this framework exports through IPC. On this image

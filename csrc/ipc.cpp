@@ -3,6 +3,7 @@
 #include <cstring>
 
 #include "igg/fault.hpp"
+#include "igg/vmm.hpp"
 
 namespace igg {
 
@@ -13,6 +14,7 @@ void* ipc_malloc(size_t bytes, MemKind kind) {
     case MemKind::FineGrained: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained)); break;
     case MemKind::Signal: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipMallocSignalMemory)); break;
     case MemKind::Uncached: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached)); break;
+    case MemKind::Vmm: return vmm_alloc(bytes, nullptr);  // zero-filled, synchronised
     default: fail("ipc_malloc: unknown memory kind ", static_cast<int>(kind));
   }
   IGG_HIP_CHECK(hipMemset(p, 0, bytes));
@@ -22,6 +24,10 @@ void* ipc_malloc(size_t bytes, MemKind kind) {
 
 void ipc_free(void* p) {
   if (!p) return;
+  if (vmm_find(p, nullptr, nullptr)) {
+    vmm_free(p);
+    return;
+  }
   (void)hipDeviceSynchronize();
   IGG_HIP_CHECK(hipFree(p));
 }

@@ -120,16 +120,24 @@ class Diffusion3D:
         import os as _os
 
         self.field_memory = (field_memory or _os.environ.get("IGG_FIELD_MEMORY", "fine")).strip().lower()
-        if self.field_memory not in ("torch", "fine"):
-            raise ValueError(f"Diffusion3D: field_memory must be 'torch' or 'fine', got {self.field_memory!r}")
+        if self.field_memory not in ("torch", "fine", "vmm"):
+            raise ValueError(f"Diffusion3D: field_memory must be 'torch', 'fine' or 'vmm', got {self.field_memory!r}")
         if self.device.type == "cuda":
             # With neighbours in other processes T/T2 may be IPC-mapped (direct
             # z, gather_ pull): no allocation may reach the IPC size limit, so
-            # a carve that would is split into one allocation per array.
+            # a carve that would is split into one allocation per array. An
+            # array that alone reaches it (1024^3 f32: 4 GiB) can never be IPC
+            # mapped; with "fine" it then lives in HIP VMM memory (MemKind 4,
+            # csrc/vmm.cpp), which gather_ maps through a file descriptor at
+            # any size instead of staging it in chunks (round 6).
+            kinds = {"torch": None, "fine": 1, "vmm": 4}
             spec = [torch.empty(shape, dtype=dtype, device="meta")] * 3
-            self.T, self.Cp, self.T2 = _carve(spec, gap=266240, kind=1 if self.field_memory == "fine" else None,
-                                              split_at=_ipc_limit() if int(gg.nprocs) > 1 else None,
-                                              device=self.device)
+            multi = int(gg.nprocs) > 1
+            big = multi and spec[0].numel() * spec[0].element_size() >= _ipc_limit()
+            self.T, self.Cp, self.T2 = _carve(spec, gap=266240, kind=kinds[self.field_memory],
+                                              split_at=_ipc_limit() if multi else None, device=self.device,
+                                              split_kind=4 if (big and self.field_memory == "fine") else None)
+            self._ipc_fields = self.field_memory == "fine" and not big  # direct z can map T/T2
         else:
             self.T, self.Cp, self.T2 = (torch.empty(shape, dtype=dtype) for _ in range(3))
         # Gaussian anomalies, evaluated in float64 a slab of x planes at a time
@@ -229,7 +237,7 @@ class Diffusion3D:
                 # Direct z sends (fused_mode bit 4) write into the neighbours'
                 # T/T2 while their kernels run: defined for fine-grained fields
                 # (docs/COHERENCE.md); torch-allocated fields only on one GPU.
-                if self.field_memory == "fine" or _grid.global_grid().nprocs == 1:
+                if getattr(self, "_ipc_fields", False) or _grid.global_grid().nprocs == 1:
                     try:
                         self._fh.set_fields(self.T.data_ptr(), self.T2.data_ptr())
                     except Exception as e:  # collective outcome: every rank gets here together
@@ -597,18 +605,20 @@ def _ipc_limit() -> int:
     return int(native.IPC_MAX_BYTES)
 
 
-def _carve(tensors, gap: int, kind=None, split_at=None, device=None):
+def _carve(tensors, gap: int, kind=None, split_at=None, device=None, split_kind=None):
     """Copies of equally sized tensors placed in one buffer ``gap`` bytes apart.
     ``kind``: None = torch's caching allocator, else a native MemKind (1 =
-    fine-grained) allocated by the runtime and handed over through DLPack.
-    ``split_at``: if the one buffer would reach this many bytes, one
-    allocation per tensor instead (the IPC size limit). Meta tensors give
-    shape and dtype only: uninitialised views on ``device``."""
+    fine-grained, 4 = HIP VMM) allocated by the runtime and handed over through
+    DLPack. ``split_at``: if the one buffer would reach this many bytes, one
+    allocation per tensor instead (the IPC size limit), of MemKind
+    ``split_kind`` if given. Meta tensors give shape and dtype only:
+    uninitialised views on ``device``."""
     nbytes = tensors[0].numel() * tensors[0].element_size()
     stride = nbytes + gap
     device = tensors[0].device if device is None else device
     if split_at is not None and stride * len(tensors) >= split_at and len(tensors) > 1:
-        return [_carve([t], 0, kind, device=device)[0] for t in tensors]
+        k = kind if split_kind is None else split_kind
+        return [_carve([t], 0, k, device=device)[0] for t in tensors]
     if kind is None:
         buf = torch.empty(stride * len(tensors), dtype=torch.uint8, device=device)
     else:

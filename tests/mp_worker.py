@@ -106,6 +106,54 @@ def scenario_gather(dev, dt):
     print(f"rank {me} gather OK")
 
 
+def scenario_gather_vmm(big_mib):
+    """gather_ of blocks in HIP VMM memory (MemKind 4, csrc/vmm.cpp): pulled in
+    place through a file descriptor at any size ('V' records), a second array
+    (a new allocation) re-imported; then gather_async_(snapshot=True) of a
+    block of ``big_mib`` MiB, staged into ONE VMM buffer instead of IPC chunks.
+    Every gathered block is checked."""
+    from igg.models.diffusion3d import native_buffer
+
+    device = _device("gpu")
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 8, 8, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+
+    def block(shape, k, p):
+        return torch.arange(math.prod(shape), dtype=torch.float32).view(shape) + 1e5 * (p + 1) + 1e6 * k
+
+    def check(G, shape, k):
+        Gc = G.cpu()
+        for p in range(nprocs):
+            c = igg.native.cart_coords(p, dims.tolist())
+            blk = Gc[c[0] * shape[0]:(c[0] + 1) * shape[0], c[1] * shape[1]:(c[1] + 1) * shape[1],
+                     c[2] * shape[2]:(c[2] + 1) * shape[2]]
+            assert torch.equal(blk, block(shape, k, p)), f"gather {k} {shape}: block of rank {p} wrong"
+
+    for k, shape in enumerate([(4, 256, 512), (4, 256, 512), (6, 128, 256)]):
+        n = math.prod(shape) * 4
+        A = native_buffer(n + 4096, 4, device)[4096:4096 + n].view(torch.float32).view(shape)  # offset inside
+        A.copy_(block(shape, k, me))
+        G = torch.zeros([int(dims[d]) * shape[d] for d in range(3)], dtype=torch.float32, device=device) \
+            if me == 0 else None
+        igg.gather_(A, G, root=0)
+        if me == 0:
+            check(G, shape, k)
+        del A, G
+    # a large snapshot: one VMM staging buffer (>= half the IPC limit), not chunks
+    nx = max(1, (int(big_mib) << 20) // (512 * 512 * 4))
+    shape = (nx, 512, 512)
+    A = block(shape, 7, me).to(device)
+    G = torch.zeros([int(dims[d]) * shape[d] for d in range(3)], dtype=torch.float32, device=device) \
+        if me == 0 else None
+    h = igg.gather_async_(A, G, root=0, snapshot=True)
+    A.fill_(-1.0)  # the snapshot was taken: A may change at once
+    h.wait()
+    if me == 0:
+        check(G, shape, 7)
+    igg.finalize_global_grid()
+    print(f"rank {me} gather vmm OK", flush=True)
+
+
 def scenario_gather_regrow():
     """gather_ (IPC pull of staged chunks, IGG_GATHER_CHUNK_BYTES set by the
     test) of blocks whose chunks are MiB-sized dedicated allocations and grow
@@ -551,6 +599,76 @@ def scenario_coherence_control(dev, nbytes, rounds, l2):
     mesh.close()
     igg.finalize_global_grid()
     print(f"rank {me} coherence control done", flush=True)
+
+
+def scenario_vmm_map(dev, nbytes):
+    """HIP VMM export of a large allocation (csrc/vmm.cpp): rank 1 creates
+    ``nbytes`` with hipMemCreate, writes a pattern at four offsets (the last
+    beyond 2 GiB), exports a POSIX fd and hands it over a Unix socket; rank 0
+    imports and maps it (bounded), reads the four regions back and copies the
+    whole allocation into its own memory (timed). hipIpcOpenMemHandle of
+    such an allocation never returns on this runtime (ipc.hpp)."""
+    import time
+    import uuid
+
+    from igg._native import native
+
+    device = _device(dev)
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 8, 8, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    nbytes = int(nbytes)
+    s = torch.cuda.current_stream(device).cuda_stream
+    chunk = 1 << 20  # bytes per pattern region
+    pat = [(torch.arange(chunk // 8, dtype=torch.int64, device=device) * 7 + k * 1000003) for k in range(4)]
+
+    def regions(size):
+        return [0, 1 << 30, (2 << 30) + (8 << 20), size - chunk]
+
+    if me == 1:
+        ptr, size = native.vmm_alloc(nbytes)
+        for k, off in enumerate(regions(size)):
+            native.copy2d([(pat[k].data_ptr(), ptr + off, 1, chunk // 8, 0, 1, 0, 1)], 8, True, s)
+        torch.cuda.synchronize()
+        fd = native.vmm_export_fd(ptr)
+        name = f"igg-vmm-{uuid.uuid4().hex}"
+        lis = native.fd_listen(name)
+        comm.all_gather_object((name, size))
+        native.fd_serve(lis, fd, 1, 60.0)
+        native.fd_close(lis)
+        native.fd_close(fd)
+        comm.barrier()  # the importer is done with the mapping
+        native.vmm_free(ptr)
+    else:
+        name, size = comm.all_gather_object(None)[1]
+        t0 = time.perf_counter()
+        fd = native.fd_fetch(name, 60.0)
+        ptr = native.vmm_import_fd(fd, size, 60.0)
+        t_map = time.perf_counter() - t0
+        for k, off in enumerate(regions(size)):
+            got = torch.empty_like(pat[k])
+            native.copy2d([(ptr + off, got.data_ptr(), 1, chunk // 8, 0, 1, 0, 1)], 8, True, s)
+            torch.cuda.synchronize()
+            assert torch.equal(got, pat[k]), f"region {k} at byte {off}: mismatch"
+        dst = torch.empty(size // 8, dtype=torch.int64, device=device)
+        rows = size // (4 << 20)
+        cp = [(ptr, dst.data_ptr(), rows, (4 << 20) // 8, (4 << 20) // 8, 1, (4 << 20) // 8, 1)]
+        native.copy2d(cp, 8, True, s)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        native.copy2d(cp, 8, True, s)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        assert torch.equal(dst[: chunk // 8], pat[0])
+        print(f"rank 0 vmm map of {size >> 20} MiB: fd + import + map {t_map * 1e3:.1f} ms, 4 regions ok, "
+              f"full copy {ms:.3f} ms ({size / ms / 1e6:.0f} GB/s)", flush=True)
+        del dst
+        native.vmm_free(ptr)
+        native.fd_close(fd)
+        comm.barrier()
+    igg.finalize_global_grid()
+    print(f"rank {me} vmm map OK", flush=True)
 
 
 def scenario_put_regrow():
