@@ -172,12 +172,15 @@ def main() -> int:
         base = [tuple(int(x) for x in c.split("/")) for c in a.candidates.split(",")]
     else:
         base = list(FUSED)
-    # one transport kind per process (parallel/halo.py enable_loopback): run
-    # the script once with IGG_TRANSPORT=rccl and once with IGG_TRANSPORT=put
+    # IGG_TRANSPORT=put|rccl: that loopback transport (run the script once per
+    # kind); auto (the default): update_halo_ chooses between both loopback
+    # transports itself on the first exchange of each shape (the library's own
+    # default path, parallel/transport_select.py auto_select)
     from igg.utils import config as _cfg
 
-    uh_forms = ((("put", "auto"),) if _cfg.transport_choice() == "put"
-                else (("rccl", "sequential"), ("rccl", "onephase")))
+    choice = _cfg.transport_choice()
+    uh_forms = ((("put", "auto"),) if choice == "put"
+                else ((("auto", "auto"),) if choice == "auto" else (("rccl", "sequential"), ("rccl", "onephase"))))
     for shape in a.shapes.split(","):
         nb = neighbours(shape)
         if a.update_halo:
@@ -211,10 +214,13 @@ def main() -> int:
                 t_uh["plain"] = min(t_uh.get("plain", float("inf")), r_.pop("plain"))
                 t_uh.update(r_)
             tpu = t_uh.pop("plain")
+            chosen = H.tuned_transports()[-1]["chosen"] if choice == "auto" and H.tuned_transports() else None
             out.setdefault("update_halo", {})[shape] = {"plain_ms": tpu, "ms": t_uh,
-                                                       "ratio": {k: v / tpu for k, v in t_uh.items()}}
+                                                       "ratio": {k: v / tpu for k, v in t_uh.items()},
+                                                       "auto_chose": chosen}
             print(f"{shape:5s} update_halo_: plain {tpu:.4f} | " +
-                  ", ".join(f"{k}={v:.4f} ({v / tpu:.4f}x)" for k, v in t_uh.items()), flush=True)
+                  ", ".join(f"{k}={v:.4f} ({v / tpu:.4f}x)" for k, v in t_uh.items()) +
+                  (f" [auto chose {chosen}]" if chosen else ""), flush=True)
         if not a.fused:
             continue
         fh = native.FusedHalo(mesh, [n, n, n], eb, nb)

@@ -496,6 +496,11 @@ def loopback_active() -> bool:
     return _loopback_comm is not None
 
 
+def loopback_one_sided() -> bool:
+    """The loopback emulation covers a one-sided shape (a node's edge or corner rank)."""
+    return _loopback_comm is not None and _loopback_one_sided
+
+
 def _use_loopback(name: str) -> None:
     global _loopback_comm
     if name not in _loopback_comms:

@@ -272,6 +272,49 @@ def test_gpu_loopback_put_transport(gpu, monkeypatch):
     igg.finalize_global_grid(finalize_MPI=False)
 
 
+def test_gpu_loopback_auto_transport(gpu, monkeypatch):
+    """IGG_TRANSPORT=auto in the loopback emulation: both loopback transports
+    exist side by side; the first exchange of each field-set signature checks
+    them against each other (periodic: the values are defined), times both and
+    keeps the faster; later exchanges reuse it, bitwise on the periodic
+    oracle. A one-sided emulated shape (a corner rank) only times them."""
+    from igg.parallel import halo as H
+
+    monkeypatch.setenv("IGG_TRANSPORT", "auto")
+    n = (10, 9, 12)
+    igg.init_global_grid(*n, periodx=1, periody=1, periodz=1, quiet=True, init_MPI=False)
+    H.enable_loopback()
+    assert H.auto_transport()
+    for _ in range(3):
+        A = encode(torch.zeros(n[0] + 1, n[1], n[2], dtype=torch.float64))
+        B = encode(torch.zeros(n[0], n[1], n[2] + 1, dtype=torch.float64))
+        refs = [A.clone(), B.clone()]
+        Ag, Bg = zero_boundaries(A.clone()).to(gpu), zero_boundaries(B.clone()).to(gpu)
+        igg.update_halo_(Ag, Bg)
+        torch.cuda.synchronize()
+        assert torch.equal(Ag.cpu(), refs[0]) and torch.equal(Bg.cpu(), refs[1])
+    log = H.tuned_transports()
+    assert len(log) == 1, log
+    assert log[0]["checked"] == {"rccl": "ok", "put": "ok"}, log
+    assert log[0]["chosen"] == min(log[0]["ms"], key=log[0]["ms"].get)
+    assert H.transport_name() == log[0]["chosen"]
+    H.check_transport()
+    # a corner rank's shape: timed only
+    H.set_halo_mode("sequential")
+    igg.get_global_grid()  # (the grid's table is rewritten by enable_loopback)
+    import igg.parallel.grid as G
+
+    G.global_grid().neighbors[:, :] = -1
+    H.enable_loopback(((False, True),) * 3)
+    X = torch.rand(n, dtype=torch.float64, device=gpu)
+    igg.update_halo_(X)
+    torch.cuda.synchronize()
+    rec = H.tuned_transports()[-1]
+    assert "timed only" in rec.get("reason", ""), rec
+    assert rec["chosen"] in ("rccl", "put")
+    igg.finalize_global_grid(finalize_MPI=False)
+
+
 @pytest.mark.parametrize("transport", ["rccl", "put"])
 def test_gpu_debug_sync_phases(gpu, monkeypatch, transport):
     """IGG_DEBUG_SYNC=1 drains and checks the stream after every phase of
