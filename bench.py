@@ -1287,6 +1287,10 @@ def main():
     dev = None if on_gpu else "cpu"
     PH.enter("model", None, deadline=900)  # allocation + stencil autotune
     model = Acoustic2D(dtype=dtype) if is2d else Diffusion3D(dtype=dtype, overlap=args.overlap, device=dev)
+    if me == 0 and getattr(model, "placement", None):
+        pl = model.placement
+        print(f"field placement: {pl['candidates']} candidate allocations, ms/step {pl['ms']} -> #{pl['chosen']}",
+              file=sys.stderr, flush=True)
     field = (lambda: model.P) if is2d else (lambda: model.T)
     sync = (lambda: _sync(comm)) if on_gpu else (lambda: None)
     A_global = None
@@ -1579,6 +1583,7 @@ def main():
                 "stencil_grid_rounds": getattr(model, "rounds", None),
                 "stencil_halo_z": getattr(model, "halo_z", None),
                 "fused_ab_ms": fused_ab,
+                "field_placement": getattr(model, "placement", None),
                 "stencil_variant": getattr(model, "variant", None),
                 "stencil_variant_ms": getattr(model, "variant_times", None),
                 "finite": finite,

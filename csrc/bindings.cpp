@@ -465,6 +465,15 @@ PYBIND11_MODULE(_igg_native, m) {
         },
         py::arg("fd"), py::arg("size"), py::arg("seconds"));
   m.def("vmm_free", [](uintptr_t p) { vmm_free(reinterpret_cast<void*>(p)); }, py::arg("ptr"));
+  m.def(
+      "range_export_fd",
+      [](uintptr_t p) {
+        void* base = nullptr;
+        size_t size = 0;
+        const int fd = range_export_fd(reinterpret_cast<void*>(p), &base, &size);
+        return py::make_tuple(fd, reinterpret_cast<uintptr_t>(base), size);
+      },
+      py::arg("ptr"), "(fd, base, size): dma-buf descriptor of the hipMalloc allocation holding ptr");
   m.def("fd_listen", &fd_listen, py::arg("name"));
   m.def("fd_serve",
         [](int listener, int fd, int clients, double seconds) {

@@ -20,6 +20,10 @@ int vmm_export_fd(void* ptr);
 void* vmm_import_fd(int fd, size_t size, double seconds);
 // Unmap / release (owner or importer).
 void vmm_free(void* ptr);
+// A dma-buf file descriptor of the whole ordinary (hipMalloc) allocation that
+// holds `ptr`, its base and size: importable with vmm_import_fd like a VMM
+// export (round 6 probe: tests/test_vmm.py).
+int range_export_fd(void* ptr, void** base, size_t* size);
 // Whether `p` lies in a mapping made by vmm_alloc (owner) / vmm_import_fd; its
 // base and mapped size.
 bool vmm_find(const void* p, void** base, size_t* size, bool* owner = nullptr);

@@ -23,6 +23,7 @@
 
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -52,9 +53,25 @@ hipMemAllocationProp prop_for(int device) {
 
 size_t round_up(size_t n, size_t g) { return (n + g - 1) / g * g; }
 
-void* map_handle(hipMemGenericAllocationHandle_t h, size_t size, int device) {
+// Placement knobs, read per allocation (benchmarks/memkind_ab.py A/Bs them in
+// one process): IGG_VMM_GRAN = "min" | "rec" (allocation granularity the size
+// is rounded to), IGG_VMM_ALIGN_MIB = alignment of the reserved VA range
+// (0 = the runtime's choice).
+bool recommended_gran() {
+  const char* e = std::getenv("IGG_VMM_GRAN");
+  return !(e && std::strcmp(e, "min") == 0);
+}
+
+size_t va_alignment(size_t gran) {
+  const char* e = std::getenv("IGG_VMM_ALIGN_MIB");
+  const size_t mib = e ? std::strtoull(e, nullptr, 10) : 2;
+  const size_t a = mib << 20;
+  return a > gran ? a : (mib ? gran : 0);
+}
+
+void* map_handle(hipMemGenericAllocationHandle_t h, size_t size, int device, size_t align) {
   void* va = nullptr;
-  IGG_HIP_CHECK(hipMemAddressReserve(&va, size, 0, nullptr, 0));
+  IGG_HIP_CHECK(hipMemAddressReserve(&va, size, align, nullptr, 0));
   IGG_HIP_CHECK(hipMemMap(va, size, 0, h, 0));
   hipMemAccessDesc acc{};
   acc.location.type = hipMemLocationTypeDevice;
@@ -91,18 +108,20 @@ bool wait_fd(int fd, short events, double seconds) {
 size_t vmm_granularity(int device) {
   hipMemAllocationProp p = prop_for(device);
   size_t g = 0;
-  IGG_HIP_CHECK(hipMemGetAllocationGranularity(&g, &p, hipMemAllocationGranularityMinimum));
+  IGG_HIP_CHECK(hipMemGetAllocationGranularity(
+      &g, &p, recommended_gran() ? hipMemAllocationGranularityRecommended : hipMemAllocationGranularityMinimum));
   return g ? g : (size_t{2} << 20);
 }
 
 void* vmm_alloc(size_t bytes, size_t* mapped) {
   int dev = 0;
   IGG_HIP_CHECK(hipGetDevice(&dev));
-  const size_t size = round_up(bytes, vmm_granularity(dev));
+  const size_t gran = vmm_granularity(dev);
+  const size_t size = round_up(bytes, gran);
   hipMemAllocationProp p = prop_for(dev);
   hipMemGenericAllocationHandle_t h{};
   IGG_HIP_CHECK(hipMemCreate(&h, size, &p, 0));
-  void* va = map_handle(h, size, dev);
+  void* va = map_handle(h, size, dev, va_alignment(gran));
   IGG_HIP_CHECK(hipMemset(va, 0, size));
   IGG_HIP_CHECK(hipDeviceSynchronize());
   {
@@ -140,7 +159,7 @@ void* vmm_import_fd(int fd, size_t size, double seconds) {
         // runtime dereferenced it: SIGSEGV, round-6 GPU run r6h.)
         int fdv = fd;
         IGG_HIP_CHECK(hipMemImportFromShareableHandle(&h, &fdv, hipMemHandleTypePosixFileDescriptor));
-        out->first = map_handle(h, size, dev);
+        out->first = map_handle(h, size, dev, va_alignment(vmm_granularity(dev)));
         out->second = h;
       },
       seconds, "vmm_import_fd (hipMemImportFromShareableHandle + map)");
@@ -168,6 +187,18 @@ void vmm_free(void* ptr) {
   // (a gather right after re-allocating an array of the same size got the
   // previous array's values, GPU run r6j). Reserved-but-unmapped VA costs no
   // memory; the process's VA space is 47+ bits.
+}
+
+int range_export_fd(void* ptr, void** base, size_t* size) {
+  hipDeviceptr_t b = nullptr;
+  size_t n = 0;
+  IGG_HIP_CHECK(hipMemGetAddressRange(&b, &n, ptr));
+  int fd = -1;
+  IGG_HIP_CHECK(hipMemGetHandleForAddressRange(&fd, b, n, hipMemRangeHandleTypeDmaBufFd, 0));
+  if (fd < 0) fail("range_export_fd: the runtime returned no file descriptor");
+  if (base) *base = b;
+  if (size) *size = n;
+  return fd;
 }
 
 bool vmm_find(const void* p, void** base, size_t* size, bool* owner) {

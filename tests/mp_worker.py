@@ -601,13 +601,15 @@ def scenario_coherence_control(dev, nbytes, rounds, l2):
     print(f"rank {me} coherence control done", flush=True)
 
 
-def scenario_vmm_map(dev, nbytes):
+def scenario_vmm_map(dev, nbytes, source="vmm"):
     """HIP VMM export of a large allocation (csrc/vmm.cpp): rank 1 creates
     ``nbytes`` with hipMemCreate, writes a pattern at four offsets (the last
     beyond 2 GiB), exports a POSIX fd and hands it over a Unix socket; rank 0
     imports and maps it (bounded), reads the four regions back and copies the
     whole allocation into its own memory (timed). hipIpcOpenMemHandle of
-    such an allocation never returns on this runtime (ipc.hpp)."""
+    such an allocation never returns on this runtime (ipc.hpp).
+    ``source="malloc"``: the allocation is torch's (hipMalloc), exported as a
+    dma-buf of its whole hipMalloc range (native.range_export_fd)."""
     import time
     import uuid
 
@@ -625,24 +627,33 @@ def scenario_vmm_map(dev, nbytes):
         return [0, 1 << 30, (2 << 30) + (8 << 20), size - chunk]
 
     if me == 1:
-        ptr, size = native.vmm_alloc(nbytes)
+        if source == "vmm":
+            ptr, size = native.vmm_alloc(nbytes)
+            fd, offset, msize = native.vmm_export_fd(ptr), 0, size
+        else:
+            buf = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+            ptr, size = buf.data_ptr(), nbytes
+            fd, base, msize = native.range_export_fd(ptr)
+            offset = ptr - base
+            print(f"rank 1 hipMalloc range {msize >> 20} MiB, tensor at offset {offset}", flush=True)
         for k, off in enumerate(regions(size)):
             native.copy2d([(pat[k].data_ptr(), ptr + off, 1, chunk // 8, 0, 1, 0, 1)], 8, True, s)
         torch.cuda.synchronize()
-        fd = native.vmm_export_fd(ptr)
         name = f"igg-vmm-{uuid.uuid4().hex}"
         lis = native.fd_listen(name)
-        comm.all_gather_object((name, size))
+        comm.all_gather_object((name, size, msize, offset))
         native.fd_serve(lis, fd, 1, 60.0)
         native.fd_close(lis)
         native.fd_close(fd)
         comm.barrier()  # the importer is done with the mapping
-        native.vmm_free(ptr)
+        if source == "vmm":
+            native.vmm_free(ptr)
     else:
-        name, size = comm.all_gather_object(None)[1]
+        name, size, msize, offset = comm.all_gather_object(None)[1]
         t0 = time.perf_counter()
         fd = native.fd_fetch(name, 60.0)
-        ptr = native.vmm_import_fd(fd, size, 60.0)
+        base = native.vmm_import_fd(fd, msize, 60.0)
+        ptr = base + offset
         t_map = time.perf_counter() - t0
         for k, off in enumerate(regions(size)):
             got = torch.empty_like(pat[k])
@@ -664,7 +675,7 @@ def scenario_vmm_map(dev, nbytes):
         print(f"rank 0 vmm map of {size >> 20} MiB: fd + import + map {t_map * 1e3:.1f} ms, 4 regions ok, "
               f"full copy {ms:.3f} ms ({size / ms / 1e6:.0f} GB/s)", flush=True)
         del dst
-        native.vmm_free(ptr)
+        native.vmm_free(base)
         native.fd_close(fd)
         comm.barrier()
     igg.finalize_global_grid()

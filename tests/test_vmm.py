@@ -10,8 +10,12 @@ from tests._mp import ROOT, run_ranks
 
 
 @pytest.mark.gpu
-def test_vmm_maps_a_3gib_allocation_across_processes():
-    outs = run_ranks(2, "vmm_map", "gpu", 3 << 30, env_extra={"IGG_FIRST_CONTACT_TIMEOUT": "60"}, timeout=150)
+@pytest.mark.parametrize("source", ["vmm", "malloc"])
+def test_vmm_maps_a_3gib_allocation_across_processes(source):
+    """source "malloc": a torch (hipMalloc) tensor exported as a dma-buf of its
+    allocation range and imported the VMM way."""
+    outs = run_ranks(2, "vmm_map", "gpu", 3 << 30, source, env_extra={"IGG_FIRST_CONTACT_TIMEOUT": "60"},
+                     timeout=150)
     line = [ln for ln in outs[0].splitlines() if "vmm map of" in ln]
     assert line, outs[0][-2000:]
     print(line[0])
