@@ -31,6 +31,7 @@ from .. import parallel  # noqa: F401
 from .._native import native
 from ..parallel import grid as _grid
 from ..parallel.halo import capture_graph, update_halo_
+from ..utils import placement as _placement
 from .diffusion3d import GRAPH_STEPS
 from ..utils.tools import coords_g, nx_g, ny_g
 
@@ -66,10 +67,20 @@ class Acoustic2D:
         fields = [P, Vx, Vy, P.clone(), Vx.clone(), Vy.clone()]
         import os as _os
 
+        self.placement = None
         if self.device.type == "cuda" and _os.environ.get("IGG_FIELD_MEMORY", "fine") != "torch":
             # One fine-grained allocation (the fused exchange stores into the
-            # neighbours' Vx2/Vy2 while their kernels run: docs/COHERENCE.md).
-            fields = _carve_fine(fields, split=int(gg.nprocs) > 1)
+            # neighbours' Vx2/Vy2 while their kernels run: docs/COHERENCE.md),
+            # the fastest of several candidates (utils/placement.py: 0.282 vs
+            # 0.300 ms/step at 8192^2 between fast and slow carves).
+            init = fields
+            nbytes = P.numel() * P.element_size()
+            k = _placement.candidate_count(gg, nbytes, sum(t.numel() * t.element_size() for t in init), self.device)
+            fields, self.placement = _placement.placed(lambda: _carve_fine(init, split=int(gg.nprocs) > 1), k,
+                                                       self._time_placements)
+            if self.placement is not None:  # the probe stepped the chosen carve: back to the initial state
+                for dst, src in zip(fields, init):
+                    dst.copy_(src)
         self.P, self.Vx, self.Vy, self.P2, self.Vx2, self.Vy2 = fields
         # P's halo cells, evaluated from the global coordinates above, equal
         # the neighbours' cells only up to rounding (periodic wrap of x_g);
@@ -88,6 +99,16 @@ class Acoustic2D:
         # remote stores must not overtake this rank's own writes to the fields
         # (switch into fused mode, restore, external edits: mark_modified).
         self._entry = True
+
+    def _time_placements(self, cands) -> list:
+        """ms per step of this model's kernel on each candidate carve
+        (P, Vx, Vy, P2, Vx2, Vy2), ping-pong (utils/placement.py)."""
+
+        def launch(c, j):
+            a, b = (c[3:], c[:3]) if j % 2 == 0 else (c[:3], c[3:])
+            self._update(*a, *b)
+
+        return _placement.time_candidates(cands, launch)
 
     def _update(self, P2, Vx2, Vy2, P, Vx, Vy) -> None:
         dev = self.device.type == "cuda"

@@ -40,6 +40,7 @@ from .. import parallel  # noqa: F401
 from ..ops import stencil
 from ..parallel import grid as _grid
 from ..parallel.halo import capture_graph, update_halo_
+from ..utils import placement as _placement
 from ..utils.tools import coords_g, nx_g, ny_g, nz_g
 
 
@@ -637,54 +638,19 @@ def _carve(tensors, gap: int, kind=None, split_at=None, device=None, split_kind=
     return out
 
 
-# Field placement probe (round 6, profiles/r6_placement/): the same carve of
-# T/Cp/T2 runs the HBM-bound sweep at one of two speeds depending on where the
-# allocator put it - 0.578 vs 0.603 ms/step at 512^3 f64, 2.42 vs 2.54 ms at
-# 1024^3 f32 - for torch, fine-grained and VMM memory alike, stable for the
-# allocation's lifetime and not predictable from its virtual address (the
-# physical pages' HBM placement). Slow ones come in runs, by allocation order:
-# the first 4 of 10 fresh 3 GiB carves of one process were slow, on another box
-# the first 7 of 8. So the model allocates up to PLACEMENT_CANDIDATES carves
-# side by side, times a short ping-pong sweep on each (a fixed plain variant;
-# it separates the two kinds by 4-5 %) and keeps the fastest: ~0.2 s at 512^3
-# f64 (48 GiB held for that time), ~0.6 s at 1024^3 f32.
-# IGG_FIELD_PLACEMENT=<k> sets the count (1 = off). Off for fields under
-# PLACEMENT_MIN_BYTES, when ranks share a GPU (their probes would time each
-# other) and where the candidates would not fit in half the free memory.
-PLACEMENT_CANDIDATES = 16
-PLACEMENT_MIN_BYTES = 256 << 20
-
-
-def _placement_count(gg, meta: torch.Tensor, device) -> int:
-    k = int(os.environ.get("IGG_FIELD_PLACEMENT", str(PLACEMENT_CANDIDATES)))
-    nbytes = meta.numel() * meta.element_size()
-    if k <= 1 or device.type != "cuda" or nbytes < PLACEMENT_MIN_BYTES:
-        return 1
-    if int(gg.nprocs) > 1:
-        from ..parallel.transport_select import _shared_device
-
-        if _shared_device(gg.comm):  # collective: every rank gets here with the same k and sizes
-            return 1
-    free, _ = torch.cuda.mem_get_info(device)
-    return max(1, min(k, int(free * 0.5) // (3 * nbytes)))
-
-
 def _placed_fields(carve, gg, meta: torch.Tensor, device):
-    """(T, Cp, T2) from ``carve()``: the fastest of ``_placement_count``
-    candidate carves by a ping-pong sweep of a fixed plain variant (the others
-    are freed), and a record {"candidates", "ms", "chosen"} (None if one)."""
-    k = _placement_count(gg, meta, device)
-    if k <= 1:
-        return carve(), None
-    cands = [carve() for _ in range(k)]
-    ms = _time_placements(cands, meta.dtype)
-    best = min(range(k), key=lambda i: ms[i])
-    return cands[best], {"candidates": k, "ms": [round(t, 5) for t in ms], "chosen": best}
+    """(T, Cp, T2) from ``carve()``, the fastest of several candidate carves
+    (utils/placement.py), and the probe's record (None without a probe)."""
+    nbytes = meta.numel() * meta.element_size()
+    k = _placement.candidate_count(gg, nbytes, 3 * nbytes, device)
+    return _placement.placed(carve, k, lambda cands: _time_placements(cands, meta.dtype))
 
 
 def _time_placements(cands, dtype, v=None, rounds: int = 3, halo_z: bool = False, steps: int = 6) -> list:
-    """Median ms per ping-pong step of each (T, Cp, T2) candidate, interleaved
-    rounds, with a fixed HBM-bound plain variant (values: T = 0, Cp = 1)."""
+    """Median ms per ping-pong step of each (T, Cp, T2) candidate with a fixed
+    plain variant (43 f64 / 14 f32 without whole-line z stores: separates fast
+    from slow carves by 4.5-5 %, benchmarks/placement_probe.py). Values: T = 0,
+    Cp = 1 (the model writes its initial conditions afterwards)."""
     if v is None:
         v = 43 if dtype == torch.float64 else 14
     if not stencil.native.diffusion3d_variant_compiled(v):
@@ -698,24 +664,13 @@ def _time_placements(cands, dtype, v=None, rounds: int = 3, halo_z: bool = False
     s = torch.cuda.current_stream()
     es = cands[0][0].element_size()
 
-    def sweep(T, Cp, T2, steps):
-        for j in range(steps):
-            dst, src = (T2, T) if j % 2 == 0 else (T, T2)
-            stencil.native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), shape, [1.0, 1.0, 1.0], 1e-3,
-                                       es, boxes, True, v, s.cuda_stream, rounds, halo_z)
+    def launch(c, j):
+        T, Cp, T2 = c
+        dst, src = (T2, T) if j % 2 == 0 else (T, T2)
+        stencil.native.diffusion3d(dst.data_ptr(), src.data_ptr(), Cp.data_ptr(), shape, [1.0, 1.0, 1.0], 1e-3,
+                                   es, boxes, True, v, s.cuda_stream, rounds, halo_z)
 
-    times = [[] for _ in cands]
-    for c in cands:
-        sweep(*c, 2)
-    for _ in range(3):
-        for i, c in enumerate(cands):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            sweep(*c, steps)
-            e1.record(s)
-            e1.synchronize()
-            times[i].append(e0.elapsed_time(e1) / steps)
-    return [sorted(t)[len(t) // 2] for t in times]
+    return _placement.time_candidates(cands, launch, steps=steps)
 
 
 def native_buffer(nbytes: int, kind: int, device) -> torch.Tensor:

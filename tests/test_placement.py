@@ -1,7 +1,7 @@
-"""Field placement probe of Diffusion3D (models/diffusion3d.py _placed_fields):
-the same T/Cp/T2 carve sweeps at one of two speeds depending on where the
-allocator put it (profiles/r6_placement/), so the model times a few candidate
-allocations and keeps the fastest."""
+"""Field placement probe (utils/placement.py): the same carve of fields sweeps
+at one of two speeds depending on where the allocator put it
+(profiles/r6_placement/), so the models time a few candidate allocations and
+keep the fastest."""
 import gc
 import weakref
 
@@ -10,6 +10,7 @@ import torch
 
 import igg
 from igg.models import diffusion3d as D
+from igg.utils import placement as PL
 
 
 class _Grid:
@@ -17,7 +18,7 @@ class _Grid:
     comm = None
 
 
-def test_placed_fields_keeps_the_fastest_and_frees_the_rest(monkeypatch):
+def test_placed_keeps_the_fastest_and_frees_the_rest():
     made = []
 
     def carve():
@@ -25,24 +26,23 @@ def test_placed_fields_keeps_the_fastest_and_frees_the_rest(monkeypatch):
         made.append([weakref.ref(t) for t in c])
         return c
 
-    monkeypatch.setattr(D, "_placement_count", lambda gg, meta, device: 3)
-    monkeypatch.setattr(D, "_time_placements", lambda cands, dtype: [0.61, 0.58, 0.60])
-    fields, rec = D._placed_fields(carve, _Grid(), torch.empty(4, device="meta"), torch.device("cpu"))
+    fields, rec = PL.placed(carve, 3, lambda cands: [0.61, 0.58, 0.60])
     gc.collect()
     assert rec == {"candidates": 3, "ms": [0.61, 0.58, 0.6], "chosen": 1}
     assert all(r() is not None for r in made[1])
     assert all(r() is None for k in (0, 2) for r in made[k])
     assert fields[0] is made[1][0]()
+    one, rec1 = PL.placed(carve, 1, lambda cands: pytest.fail("no probe with one candidate"))
+    assert rec1 is None and len(made) == 4
 
 
-def test_placement_count_off_cases(monkeypatch):
-    big = torch.empty((1024, 1024, 64), dtype=torch.float64, device="meta")  # 512 MiB
-    small = torch.empty((64, 64, 64), dtype=torch.float64, device="meta")
+def test_candidate_count_off_cases(monkeypatch):
+    big, small = 512 << 20, 2 << 20
     monkeypatch.delenv("IGG_FIELD_PLACEMENT", raising=False)
-    assert D._placement_count(_Grid(), big, torch.device("cpu")) == 1  # host fields
-    assert D._placement_count(_Grid(), small, torch.device("cuda", 0)) == 1  # below PLACEMENT_MIN_BYTES
+    assert PL.candidate_count(_Grid(), big, 3 * big, torch.device("cpu")) == 1  # host fields
+    assert PL.candidate_count(_Grid(), small, 3 * small, torch.device("cuda", 0)) == 1  # below MIN_FIELD_BYTES
     monkeypatch.setenv("IGG_FIELD_PLACEMENT", "1")
-    assert D._placement_count(_Grid(), big, torch.device("cuda", 0)) == 1  # switched off
+    assert PL.candidate_count(_Grid(), big, 3 * big, torch.device("cuda", 0)) == 1  # switched off
 
 
 def test_cpu_model_has_no_placement_record():
@@ -55,8 +55,8 @@ def test_cpu_model_has_no_placement_record():
 
 
 @pytest.mark.gpu
-def test_placement_probe_on_the_headline_size(monkeypatch):
-    """512^3 f64 (the bench's shape): four candidate carves timed, the fastest
+def test_placement_probe_diffusion_headline_size(monkeypatch):
+    """512^3 f64 (the bench's shape): CANDIDATES carves timed, the fastest
     kept; the chosen fields hold the initial conditions (the probe's scribbles
     are overwritten) and step bitwise like a model without the probe."""
     monkeypatch.delenv("IGG_FIELD_PLACEMENT", raising=False)
@@ -64,7 +64,7 @@ def test_placement_probe_on_the_headline_size(monkeypatch):
     try:
         m = D.Diffusion3D(variant=43)
         rec = m.placement
-        assert rec is not None and rec["candidates"] == D.PLACEMENT_CANDIDATES, rec
+        assert rec is not None and rec["candidates"] == PL.CANDIDATES, rec
         assert rec["ms"][rec["chosen"]] == min(rec["ms"])
         print(f"placement: {rec}")
         monkeypatch.setenv("IGG_FIELD_PLACEMENT", "1")
@@ -75,5 +75,33 @@ def test_placement_probe_on_the_headline_size(monkeypatch):
         ref.run(6)
         torch.cuda.synchronize()
         assert torch.equal(m.T, ref.T)
+    finally:
+        igg.finalize_global_grid(finalize_MPI=False)
+
+
+@pytest.mark.gpu
+def test_placement_probe_acoustic(monkeypatch):
+    """8192^2 f32 acoustic: the probe steps the candidates with the model's own
+    kernel; the chosen carve is reset to the initial state and steps bitwise
+    like a model without the probe."""
+    from igg.models.acoustic2d import Acoustic2D
+
+    monkeypatch.delenv("IGG_FIELD_PLACEMENT", raising=False)
+    igg.init_global_grid(8192, 8192, 1, quiet=True, init_MPI=False)
+    try:
+        m = Acoustic2D()
+        rec = m.placement
+        assert rec is not None and rec["candidates"] == PL.CANDIDATES, rec
+        assert rec["ms"][rec["chosen"]] == min(rec["ms"])
+        print(f"placement: {rec}")
+        monkeypatch.setenv("IGG_FIELD_PLACEMENT", "1")
+        ref = Acoustic2D()
+        assert ref.placement is None
+        for a, b in ((m.P, ref.P), (m.Vx, ref.Vx), (m.Vy, ref.Vy), (m.P2, ref.P2), (m.Vx2, ref.Vx2), (m.Vy2, ref.Vy2)):
+            assert torch.equal(a, b)
+        m.run(6)
+        ref.run(6)
+        torch.cuda.synchronize()
+        assert torch.equal(m.P, ref.P) and torch.equal(m.Vx, ref.Vx) and torch.equal(m.Vy, ref.Vy)
     finally:
         igg.finalize_global_grid(finalize_MPI=False)
