@@ -12,10 +12,14 @@ its speed for its lifetime, and its virtual address does not predict the
 speed. Slow allocations come in runs by allocation order: the first 4-7 of a
 fresh process's carves were slow on some boxes, 0-2 on others.
 
-So a model allocates up to ``CANDIDATES`` carves side by side, times a short
+So a model allocates ``CANDIDATES`` carves side by side, times a short
 ping-pong sweep of its own kernel on each, keeps the fastest and frees the
-rest. ``IGG_FIELD_PLACEMENT=<k>`` sets the count; ``1`` turns the probe off.
-The probe is also off in three cases:
+rest. If all of them are alike (within ``SPREAD``) it cannot tell a box of
+only slow pages from one of only fast pages, so it allocates more, another
+batch at a time, up to ``MAX_CANDIDATES`` or half the free device memory, and
+stops as soon as a batch shows two speeds. ``IGG_FIELD_PLACEMENT=<k>`` probes
+exactly k candidates; ``1`` turns the probe off. The probe is also off in
+three cases:
 
 * fields under ``MIN_FIELD_BYTES``;
 * ranks that share a GPU: their probes would time each other;
@@ -31,23 +35,28 @@ import os
 import torch
 
 CANDIDATES = 16
+MAX_CANDIDATES = 64
+SPREAD = 1.025  # fast and slow carves differ by 4.5-6 %; the noise of one probe is < 0.5 %
 MIN_FIELD_BYTES = 256 << 20
 
 
-def candidate_count(gg, field_bytes: int, carve_bytes: int, device) -> int:
-    """Number of candidate carves to probe (1 = no probe). Collective on a
-    multi-rank grid: every rank must call it at the same point with the same
-    environment."""
-    k = int(os.environ.get("IGG_FIELD_PLACEMENT", str(CANDIDATES)))
+def candidate_count(gg, field_bytes: int, carve_bytes: int, device):
+    """``(batch, limit)``: candidate carves per probe batch and in total
+    (``(1, 1)`` = no probe). Collective on a multi-rank grid: every rank must
+    call it at the same point with the same environment."""
+    env = os.environ.get("IGG_FIELD_PLACEMENT")
+    k = int(env) if env is not None else CANDIDATES
     if k <= 1 or torch.device(device).type != "cuda" or field_bytes < MIN_FIELD_BYTES:
-        return 1
+        return 1, 1
     if int(gg.nprocs) > 1:
         from ..parallel.transport_select import _shared_device
 
         if _shared_device(gg.comm):
-            return 1
+            return 1, 1
     free, _ = torch.cuda.mem_get_info(device)
-    return max(1, min(k, int(free * 0.5) // max(1, carve_bytes)))
+    fit = max(1, int(free * 0.5) // max(1, carve_bytes))
+    limit = min(fit, k if env is not None else MAX_CANDIDATES)
+    return min(k, limit), limit
 
 
 def time_candidates(cands, launch, steps: int = 6, rounds: int = 3, warm: int = 2) -> list:
@@ -71,14 +80,30 @@ def time_candidates(cands, launch, steps: int = 6, rounds: int = 3, warm: int = 
     return [sorted(t)[len(t) // 2] for t in times]
 
 
-def placed(carve, count: int, timer):
-    """``(fields, record)``: the fastest of ``count`` carves by
-    ``timer(cands) -> [ms]``. The other carves are released when this
-    returns. ``record`` is ``{"candidates", "ms", "chosen"}``, or None when
-    ``count`` is 1."""
-    if count <= 1:
+def placed(carve, count, timer):
+    """``(fields, record)``: the fastest of the carves from ``carve()`` by
+    ``timer(cands) -> [ms]``. ``count`` is ``(batch, limit)`` from
+    ``candidate_count`` (or an int: one batch). Later batches are timed
+    together with the best so far, so every decision compares times from one
+    run. The other carves are released when this returns. ``record`` is
+    ``{"candidates", "batches", "ms", "chosen"}``, or None without a probe."""
+    batch, limit = (count, count) if isinstance(count, int) else count
+    if batch <= 1:
         return carve(), None
-    cands = [carve() for _ in range(count)]
-    ms = timer(cands)
-    best = min(range(count), key=lambda i: ms[i])
-    return cands[best], {"candidates": count, "ms": [round(t, 5) for t in ms], "chosen": best}
+    cands, ms, batches = [], [], 0
+    while True:
+        new = [carve() for _ in range(min(batch, limit - len(cands)))]
+        if cands:
+            best = min(range(len(ms)), key=lambda i: ms[i])
+            t = timer([cands[best]] + new)
+            ms[best] = t[0]
+            ms += t[1:]
+        else:
+            ms = list(timer(new))
+        cands += new
+        batches += 1
+        if max(ms) >= SPREAD * min(ms) or len(cands) >= limit:
+            break
+    best = min(range(len(ms)), key=lambda i: ms[i])
+    return cands[best], {"candidates": len(cands), "batches": batches, "ms": [round(t, 5) for t in ms],
+                         "chosen": best}
