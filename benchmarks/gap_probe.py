@@ -8,7 +8,7 @@ one buffer, the relative placement decides; if it follows the buffer, the
 pages do.
 
 Usage: python benchmarks/gap_probe.py [--n 512] [--dtype float64] [--k 6]
-       [--gaps 0,65536,266240,1048576,2363392,16777216] [--kinds 1,5,6]
+       [--gaps 0,65536,266240,1048576,2363392,16777216] [--kinds 1,5]
 """
 import argparse
 import os
@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--gaps", default="0,65536,266240,1048576,2363392,16777216")
     ap.add_argument("--offset", type=int, default=0, help="extra offset of T from the buffer start")
     ap.add_argument("--kinds", default="1", help="native MemKinds of the buffers, cycled (ipc.hpp: 0 coarse, "
-                    "1 fine, 4 VMM, 5 contiguous, 6 fine+contiguous)")
+                    "1 fine, 4 VMM, 5 contiguous)")
     args = ap.parse_args()
     import torch
 

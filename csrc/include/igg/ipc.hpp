@@ -24,8 +24,8 @@ enum class MemKind : int {
   Signal = 2,      // hipMallocSignalMemory
   Uncached = 3,    // hipDeviceMallocUncached (coherent across devices, bypasses L2)
   Vmm = 4,         // hipMemCreate + map (vmm.hpp): exportable at any size (a file descriptor)
-  Contiguous = 5,  // hipDeviceMallocContiguous (physically contiguous, coarse-grained)
-  FineContiguous = 6,  // hipDeviceMallocFinegrained | hipDeviceMallocContiguous
+  Contiguous = 5,  // hipDeviceMallocContiguous (physically contiguous, coarse-grained; the runtime
+                   // refuses it combined with fine-grained: 'invalid argument')
 };
 
 // Largest allocation this framework exports through IPC. On this image

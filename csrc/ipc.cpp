@@ -16,9 +16,6 @@ void* ipc_malloc(size_t bytes, MemKind kind) {
     case MemKind::Uncached: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached)); break;
     case MemKind::Vmm: return vmm_alloc(bytes, nullptr);  // zero-filled, synchronised
     case MemKind::Contiguous: IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous)); break;
-    case MemKind::FineContiguous:
-      IGG_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained | hipDeviceMallocContiguous));
-      break;
     default: fail("ipc_malloc: unknown memory kind ", static_cast<int>(kind));
   }
   IGG_HIP_CHECK(hipMemset(p, 0, bytes));
