@@ -66,6 +66,34 @@ def test_candidate_count_off_cases(monkeypatch):
     assert PL.candidate_count(_Grid(), big, 3 * big, torch.device("cuda", 0)) == (1, 1)  # switched off
 
 
+class _Comm:
+    def __init__(self, devs):
+        self.devs = devs
+
+    def all_gather_object(self, obj):
+        return self.devs
+
+
+def test_candidate_count_is_off_when_ranks_share_a_gpu(monkeypatch):
+    """Multi-rank: a shared device turns the probe off on every rank (the probes
+    would time each other); distinct devices keep it, sized by free memory."""
+    monkeypatch.delenv("IGG_FIELD_PLACEMENT", raising=False)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 0)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda device=None: (288 << 30, 288 << 30))
+    g = _Grid()
+    g.nprocs = 2
+    import socket
+
+    host = socket.gethostname()
+    g.comm = _Comm([(host, 0), (host, 0)])
+    big = 1 << 30
+    assert PL.candidate_count(g, big, 3 * big, torch.device("cuda", 0)) == (1, 1)
+    g.comm = _Comm([(host, 0), (host, 1)])
+    assert PL.candidate_count(g, big, 3 * big, torch.device("cuda", 0)) == (PL.CANDIDATES, 48)  # 144 GiB / 3 GiB
+    monkeypatch.setenv("IGG_FIELD_PLACEMENT", "5")
+    assert PL.candidate_count(g, big, 3 * big, torch.device("cuda", 0)) == (5, 5)  # an explicit count: no escalation
+
+
 def test_cpu_model_has_no_placement_record():
     igg.init_global_grid(8, 8, 8, quiet=True, init_MPI=False, device_type="none")
     try:
