@@ -97,7 +97,10 @@ FUSED_ZUNPACK_F32 = ((44, 64, 4), (14, 64, 3))
 #   (14, 8, 3) f32 x/xy (m24 = 8|16), (44, 44, 4) / (44, 12, 4) f32 corner
 #   (9, 72, 3) / (42, 72, 2): the round-5 z-unpack corner forms (no record yet;
 #   right behind the record's front so a spent budget still times them)
-FUSED_WIN_ORDER = ((9, 8, 2), (9, 0, 2), (9, 8, 3), (42, 12, 2), (42, 9, 2), (9, 0, 3), (9, 72, 3), (42, 72, 2),
+#   (40, 8, 2) / (40, 0, 2): x+ / xy+ f64 since round 6 (plain waves on the
+#   vector march, igg/vsweep.hpp: 1.012-1.017x, profiles/r6_vsweep/)
+FUSED_WIN_ORDER = ((9, 8, 2), (9, 0, 2), (40, 8, 2), (40, 0, 2), (9, 8, 3), (42, 12, 2), (42, 9, 2), (9, 0, 3),
+                   (9, 72, 3), (42, 72, 2),
                    (42, 8, 2), (14, 8, 3), (44, 44, 4), (44, 12, 4), (44, 72, 4), (42, 4, 2), (0, 12, 3), (42, 0, 2),
                    (40, 12, 2))
 

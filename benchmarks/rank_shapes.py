@@ -89,12 +89,25 @@ def main() -> int:
     hz = bool(a.halo_z)
     dt = getattr(torch, a.dtype)
     igg.init_global_grid(n, n, n, periodx=1, periody=1, periodz=1, quiet=True)
-    from igg.models.diffusion3d import native_buffer
+    from igg.models import diffusion3d as D
+    from igg.parallel import grid as _grid
+    from igg.utils import placement as PL
 
-    # fine-grained fields in one allocation, as the model allocates them
+    # fine-grained fields in one allocation, as the model allocates them, on
+    # the fastest of the placement probe's candidates (utils/placement.py;
+    # IGG_FIELD_PLACEMENT=1: whatever the allocator gives)
     nbytes = n * n * n * dt.itemsize
-    buf = native_buffer(3 * nbytes + 2 * 266240, 1, torch.device("cuda", 0))
-    T, T2, Cp = (buf[k * (nbytes + 266240):k * (nbytes + 266240) + nbytes].view(dt).view(n, n, n) for k in range(3))
+
+    def views(b):
+        return [b[k * (nbytes + 266240):k * (nbytes + 266240) + nbytes].view(dt).view(n, n, n) for k in range(3)]
+
+    cnt = PL.candidate_count(_grid.global_grid(), nbytes, 3 * nbytes, torch.device("cuda", 0))
+    buf, placement = PL.placed(lambda: D.native_buffer(3 * nbytes + 2 * 266240, 1, torch.device("cuda", 0)), cnt,
+                               lambda cands: D._time_placements([(v[0], v[2], v[1]) for v in map(views, cands)], dt))
+    if placement:
+        print(f"field placement: {placement['candidates']} candidates, chosen {placement['chosen']} "
+              f"({min(placement['ms']):.5f} vs max {max(placement['ms']):.5f} ms)", flush=True)
+    T, T2, Cp = views(buf)
     g = torch.Generator(device="cpu").manual_seed(0)
     T.copy_(torch.rand(n, n, n, generator=g, dtype=torch.float64).to(dt))
     T2.copy_(T)
@@ -167,7 +180,7 @@ def main() -> int:
     best_plain = min(pl, key=pl.get)
     print(f"n={n}^3 {a.dtype}: best plain {best_plain} {pl[best_plain]:.4f} ms "
           f"({3 * n ** 3 * eb / pl[best_plain] / 1e6:.0f} GB/s)", flush=True)
-    out = {"n": n, "dtype": a.dtype, "plain": pl, "best_plain": best_plain, "shapes": {}}
+    out = {"n": n, "dtype": a.dtype, "placement": placement, "plain": pl, "best_plain": best_plain, "shapes": {}}
     if a.candidates:
         base = [tuple(int(x) for x in c.split("/")) for c in a.candidates.split(",")]
     else:

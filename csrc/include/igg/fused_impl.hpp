@@ -28,6 +28,7 @@
 #include "igg/devsync.hpp"
 #include "igg/stencil.hpp"
 #include "igg/sysstore.hpp"
+#include "igg/vsweep.hpp"
 
 
 namespace igg {
@@ -274,6 +275,23 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
   if (nv <= 0 || xs >= xe) return;
   const int64_t hi2 = n2 - 1;
   if (zt >= hi2) return;
+  // A wave that exchanges nothing runs the plain vector march (igg/vsweep.hpp):
+  // 15 % less VALU than this loop's plain form, 2 % per step for tiling 11
+  // (profiles/r6_vsweep/). FEAT 512 (lane-distributed edge loads) only chose
+  // how this loop's plain form fetched the segment edges: ignored there. Not
+  // for 8-wave workgroups (tiling 43's full-row tiles): at <= 256 VGPRs the
+  // vector march spills (4 VGPRs, 20 B scratch) and ran 4.5 % slower. Not for
+  // the side-only z forms (tiling 9, ZSIDES): there the 2x2x2 corner step got
+  // 0.6 % slower (same-box A/B, profiles/r6_vsweep/). f64 only: the f32
+  // restrict-form plain variants ran 2.5-6 % slower relative to the vector
+  // kernel with it (1024^3).
+  constexpr int NOT_PLAIN =
+      1 | 2 | 4 | 8 | 64 | 128 | 256 | 4096 | 8192 | 16384 | 32768 | 65536 | 131072 | ZSIDES;
+  if constexpr ((FEAT & NOT_PLAIN) == 0 && BY * BZ <= 4 && sizeof(T) == 8) {
+    v_sweep<T, RY, VZ, PF, true, (FEAT & HZ) != 0, true>(t2, t, cpp, n0, n1, n2, xs, xe, y0, nv, zt, 1, hi2, a.rdx2,
+                                                         a.rdy2, a.rdz2, a.dtlam, a.zh_lo != 0, a.zh_hi != 0);
+    return;
+  }
   const int64_t z0 = zt + lane * VZ;
   const int64_t zhi_v = ((hi2 - 1) / VZ) * VZ;
   const int64_t zc = min(z0, zhi_v);
