@@ -87,7 +87,12 @@ def build(jobs: int | None = None, debug: bool = False, asan: bool = False, verb
         flags += ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
     if probes:
         flags += ["-DIGG_PROBES"]
+    # measurement builds only (e.g. "-DIGG_WAVES_PER_EU=2"); part of the object tag
+    extra = os.environ.get("IGG_EXTRA_FLAGS", "").split()
+    flags += extra
     tag = ("dbg" if debug else "opt") + ("-asan" if asan else "") + ("-probes" if probes else "") + "-fpc0"
+    if extra:
+        tag += "-x" + "".join(c for c in "".join(extra) if c.isalnum())
     hdr_t = _headers_mtime()
     todo = []
     objs = []

@@ -677,8 +677,13 @@ hx_sweep(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
 // because it changes the hot loop's schedule. The test is wave-uniform, so the
 // dispatch is a scalar branch; results are unchanged (the skipped features are
 // no-ops for such a wave).
+#ifdef IGG_WAVES_PER_EU  // measurement builds (build.py IGG_EXTRA_FLAGS)
+#define IGG_HX_OCC_ATTR __attribute__((amdgpu_waves_per_eu(IGG_WAVES_PER_EU)))
+#else
+#define IGG_HX_OCC_ATTR
+#endif
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT = 207>
-__global__ void __launch_bounds__(64 * BY * BZ)
+__global__ void __launch_bounds__(64 * BY * BZ) IGG_HX_OCC_ATTR
 diffusion3d_hx_kernel(T* __restrict__ t2, const T* __restrict__ t, const T* __restrict__ cpp,
                       const T* __restrict__ xi0, const T* __restrict__ xi1, const T* __restrict__ yi0,
                       const T* __restrict__ yi1, const T* __restrict__ zi0, const T* __restrict__ zi1,

@@ -149,8 +149,15 @@ __device__ __forceinline__ typename VecOf<T, VZ>::type vload(const T* p) {
 // HZ: the whole-line z-edge store form (DiffusionArgs::halo_z), a separate
 // instantiation - its extra branches cost tiling 11 2.7 % where the partial
 // edge stores cost it nothing, so the autotune times both forms.
+// IGG_WAVES_PER_EU (measurement builds, build.py IGG_EXTRA_FLAGS): a minimum
+// occupancy for the register allocator (profiles/r6_vsweep/).
+#ifdef IGG_WAVES_PER_EU
+#define IGG_OCC_ATTR __attribute__((amdgpu_waves_per_eu(IGG_WAVES_PER_EU)))
+#else
+#define IGG_OCC_ATTR
+#endif
 template <typename T, int BY, int RY, int VZ, bool PF, bool NT, int BZ, bool HZ>
-__global__ void __launch_bounds__(64 * BY * BZ)
+__global__ void __launch_bounds__(64 * BY * BZ) IGG_OCC_ATTR
 diffusion3d_vkernel(const KArgs<T> a, const BoxTable bt) {
   using V = typename VecOf<T, VZ>::type;
   constexpr int W = 64 * VZ * BZ;  // block tile width along z
