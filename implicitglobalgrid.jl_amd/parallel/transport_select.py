@@ -67,15 +67,22 @@ def _agree_max(comm, v: float) -> float:
 
 
 def _check_and_time(fields, names, switch, comm, rank: int, nranks: int, ref, steps: int,
-                    skip: dict | None = None, compare: bool = True) -> tuple[dict, dict]:
+                    skip: dict | None = None, compare: bool = True, rounds: int = 3,
+                    reswitch=None) -> tuple[dict, dict]:
     """For each transport name: ``switch(name)`` (collective), one
     ``update_halo_`` of probes shaped like ``fields``, compared with ``ref``
     (the probes after the reference exchange; None: every candidate must equal
     the first one that passed; ``compare`` False: no comparison, the exchange
-    must only complete), then ``steps`` timed exchanges (MAX over ranks).
-    Every outcome is agreed over ranks. Returns (checked, ms)."""
+    must only complete). Then the ones that passed are timed in ``rounds``
+    interleaved rounds of ``steps`` exchanges each (the MAX over ranks per
+    round, the best round kept), so no candidate is favoured by running first
+    or last. ``reswitch`` (default ``switch``) moves between the checked
+    transports in those rounds (select_transport: without ending the
+    schedule caches each time). Every outcome is agreed over ranks. Returns
+    (checked, ms)."""
     checked, ms = {}, {}
     first_ok = None
+    probes = {}
     for name in names:
         if skip and name in skip:
             checked[name] = skip[name]
@@ -113,18 +120,21 @@ def _check_and_time(fields, names, switch, comm, rank: int, nranks: int, ref, st
             continue
         if ref is None and first_ok is None:
             first_ok = [x.clone() for x in X]
-        # timing: the probes again (the caller's fields stay untouched)
-        _halo.update_halo_(*X)
-        torch.cuda.synchronize()
-        if comm is not None:
-            comm.barrier()
-        t0 = time.perf_counter()
-        for _ in range(max(1, int(steps))):
-            _halo.update_halo_(*X)
-        torch.cuda.synchronize()
-        dt = _agree_max(comm, time.perf_counter() - t0)
-        ms[name] = round(dt / max(1, int(steps)) * 1e3, 5)
-        del X
+        probes[name] = X  # timed below on the probes (the caller's fields stay untouched)
+    n = max(1, int(steps))
+    for _ in range(max(1, int(rounds))):
+        for name, X in probes.items():
+            (reswitch or switch)(name)
+            _halo.update_halo_(*X)  # warm: the switch may have left another transport's state behind
+            torch.cuda.synchronize()
+            if comm is not None:
+                comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                _halo.update_halo_(*X)
+            torch.cuda.synchronize()
+            dt = _agree_max(comm, time.perf_counter() - t0)
+            ms[name] = min(ms.get(name, float("inf")), round(dt / n * 1e3, 5))
     return checked, ms
 
 
@@ -170,7 +180,7 @@ def select_transport(A: torch.Tensor, candidates=DEFAULT_CANDIDATES, steps: int 
         skip = {n: "skipped: ranks share a GPU (RCCL refuses duplicate devices)"
                 for n in candidates if shared and n in ("rccl", "torch")}
         out["checked"], out["ms"] = _check_and_time([A], list(candidates), _halo.set_transport, comm, int(gg.me),
-                                                    int(gg.nprocs), [R], steps, skip)
+                                                    int(gg.nprocs), [R], steps, skip, reswitch=_halo.use_transport)
         del R
     ok = [n for n in candidates if out["checked"].get(n) == "ok"]
     if not ok:
@@ -185,7 +195,8 @@ def select_transport(A: torch.Tensor, candidates=DEFAULT_CANDIDATES, steps: int 
     return out
 
 
-# auto_select: timed exchanges per candidate (after one untimed warm-up each)
+# auto_select: timed exchanges per candidate and round (3 interleaved rounds,
+# each after one untimed warm-up exchange; the best round counts)
 AUTO_STEPS = 5
 
 
