@@ -645,6 +645,7 @@ PYBIND11_MODULE(_igg_native, m) {
            py::arg("snapshot") = false)
       .def("wait", [](PullGatherer& g, uintptr_t s) { g.wait(as_stream(s)); }, py::arg("stream"))
       .def_property_readonly("pending", &PullGatherer::pending)
+      .def_property_readonly("last_kind", [](const PullGatherer& g) { return std::string(g.last_kind()); })
       .def("free", &PullGatherer::free);
   m.def("gather_reorder", [](uintptr_t src, uintptr_t dst, const Int3& s, const Int3& dims,
                              int eb, uintptr_t stream) {

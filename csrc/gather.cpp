@@ -118,13 +118,45 @@ PullGatherer::PullGatherer(int rank, int nranks, AllGather allgather)
   mapped_vmm_.assign(nranks, 0);
 }
 
-std::string PullGatherer::vmm_record(void* base, size_t size, uint64_t off) {
+namespace {
+uint64_t buffer_id(void* p) {
+  unsigned long long id = 0;
+  IGG_HIP_CHECK(hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(p)));
+  return id;
+}
+
+int export_fd(void* base, bool dmabuf) {
+  return dmabuf ? range_export_fd(base, nullptr, nullptr) : vmm_export_fd(base);
+}
+}  // namespace
+
+// IGG_GATHER_DMABUF=0: an ordinary allocation of 2 GiB or more is staged into
+// the VMM buffer (one copy) instead of being exported as a dma-buf.
+bool dmabuf_gather() {
+  static const bool on = [] {
+    const char* e = std::getenv("IGG_GATHER_DMABUF");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+std::string PullGatherer::vmm_record(void* base, size_t size, uint64_t off, bool dmabuf) {
+  const uint64_t id = dmabuf ? buffer_id(base) : 0;
   int k = 0;
   while (k < static_cast<int>(vexp_.size()) && vexp_[k].base != base) ++k;
+  if (k < static_cast<int>(vexp_.size()) && (vexp_[k].dmabuf != dmabuf || vexp_[k].buffer_id != id)) {
+    // another allocation at this address now: retire the old export
+    fd_close(vexp_[k].listener);
+    fd_close(vexp_[k].fd);
+    vexp_.erase(vexp_.begin() + k);
+    k = static_cast<int>(vexp_.size());
+  }
   if (k == static_cast<int>(vexp_.size())) {
     VmmExport e;
     e.base = base;
-    e.fd = vmm_export_fd(base);
+    e.dmabuf = dmabuf;
+    e.buffer_id = id;
+    e.fd = export_fd(base, dmabuf);
     static int serial = 0;
     e.name = "igg-gather-" + std::to_string(::getpid()) + "-" + std::to_string(rank_) + "-" + std::to_string(serial++);
     e.listener = fd_listen(e.name);
@@ -242,6 +274,7 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
     inject_fail("gather_export");
     std::string rec;  // after the event handle: 'D' handle offset | 'C' nchunks planes/chunk handles...
     cur_vexp_ = -1;
+    last_kind_ = "root";
     if (rank_ != root) {
       void* base = nullptr;
       size_t size = 0;
@@ -253,9 +286,17 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
       const size_t abytes = plane * static_cast<size_t>(a.size[0]);
       // snapshot: `a` may change as soon as start() returns, so it is copied
       // into the staging chunks in any case (the chunks are the snapshot).
+      int dev = 0;
+      IGG_HIP_CHECK(hipGetDevice(&dev));
       if (a_vmm && !snapshot) {
         // a VMM allocation: exportable at any size, pulled in place
         rec = vmm_record(base, size, a.ptr - reinterpret_cast<uintptr_t>(base));
+        last_kind_ = "vmm";
+      } else if (!a_vmm && !snapshot && size >= IPC_MAX_BYTES && !forced && dmabuf_gather() &&
+                 size % vmm_granularity(dev) == 0) {
+        // an ordinary allocation above the IPC limit: its dma-buf, pulled in place
+        rec = vmm_record(base, size, a.ptr - reinterpret_cast<uintptr_t>(base), true);
+        last_kind_ = "dmabuf";
       } else if ((snapshot || size >= IPC_MAX_BYTES) && !forced && vmm_staging() && abytes >= IPC_MAX_BYTES / 2) {
         // a large snapshot / an unexportable allocation: ONE VMM staging
         // buffer (grow-only; a grown-out one is retired, its export name dies
@@ -267,6 +308,7 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
         IGG_HIP_CHECK(hipMemcpyAsync(vstage_, reinterpret_cast<const void*>(a.ptr), abytes, hipMemcpyDeviceToDevice,
                                      stream));
         rec = vmm_record(vstage_, vstage_bytes_, 0);
+        last_kind_ = "vmm-staging";
       } else if (snapshot || size >= IPC_MAX_BYTES || (forced && plane * a.size[0] > cap)) {
         // Stage into exportable chunks of whole planes (class comment).
         const int64_t ppc = std::max<int64_t>(1, static_cast<int64_t>(cap / std::max<size_t>(plane, 1)));
@@ -289,6 +331,7 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
           stage_bytes_ = cb;
         }
         rec.push_back('C');
+        last_kind_ = "chunks";
         put_u32(rec, static_cast<uint32_t>(nch));
         put_u32(rec, static_cast<uint32_t>(ppc));
         for (int64_t k = 0; k < nch; ++k) {
@@ -300,6 +343,7 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
       } else {
         const uint64_t off = a.ptr - reinterpret_cast<uintptr_t>(base);
         rec.push_back('D');
+        last_kind_ = "ipc";
         rec += ipc_get_handle(base);
         rec.append(reinterpret_cast<const char*>(&off), sizeof(off));
       }
@@ -448,7 +492,13 @@ void PullGatherer::start(const Field& a, void* dst, int root, const Int3& dims, 
       // the root asked for this rank's VMM descriptor: hand it over (bounded)
       if (need.size() == static_cast<size_t>(nranks_) && need[rank_] == '1') {
         if (cur_vexp_ < 0) fail("gather_async: the root asked for a VMM export this rank did not publish");
-        fd_serve(vexp_[cur_vexp_].listener, vexp_[cur_vexp_].fd, 1, first_contact_timeout());
+        VmmExport& e = vexp_[cur_vexp_];
+        if (e.fd < 0) e.fd = export_fd(e.base, e.dmabuf);  // served and closed before: export again
+        fd_serve(e.listener, e.fd, 1, first_contact_timeout());
+        if (e.dmabuf) {  // the root holds its own reference now; ours would keep a freed array alive
+          fd_close(e.fd);
+          e.fd = -1;
+        }
       }
       const std::string& rec = all[root];
       if (rec.size() != EH * (1 + used_)) fail("gather_async: malformed handles from the root");

@@ -89,6 +89,8 @@ class PullGatherer {
   void start(const Field& a, void* dst, int root, const Int3& dims, hipStream_t stream, bool snapshot = false);
   void wait(hipStream_t stream);
   bool pending() const { return pending_; }
+  // "root", "ipc", "chunks", "vmm", "dmabuf" or "vmm-staging": how start() published this rank's block
+  const char* last_kind() const { return last_kind_; }
   void free();
 
  private:
@@ -114,10 +116,19 @@ class PullGatherer {
   // offset), and a large snapshot is staged into ONE grow-only VMM buffer
   // instead of IPC chunks. The root maps each once (cached by socket name)
   // and pulls it as one block.
+  // Also published this way: an `a` in an ordinary hipMalloc allocation of
+  // 2 GiB or more (above the IPC limit), as a dma-buf of the whole allocation
+  // (range_export_fd; IGG_GATHER_DMABUF=0: the VMM staging copy instead). A
+  // freed-and-reallocated range at the same address is told apart by its
+  // runtime buffer id: a new id makes a new export (new name: the root maps
+  // again). The descriptor is closed once served (it holds a reference to the
+  // allocation) and exported again if the root asks again.
   struct VmmExport {
     void* base = nullptr;
     int listener = -1, fd = -1;
     std::string name;
+    bool dmabuf = false;
+    uint64_t buffer_id = 0;
   };
   std::vector<VmmExport> vexp_;
   int cur_vexp_ = -1;           // the export published by the pending gather (non-root)
@@ -125,9 +136,10 @@ class PullGatherer {
   size_t vstage_bytes_ = 0;
   std::vector<void*> vretired_;
   std::vector<char> mapped_vmm_;  // root: mapped_[p] holds VMM imports (vmm_free) rather than IPC maps
-  std::string vmm_record(void* base, size_t size, uint64_t off);
+  std::string vmm_record(void* base, size_t size, uint64_t off, bool dmabuf = false);
   void close_mapped(int p);
   void free_vmm();
+  const char* last_kind_ = "";  // how this rank published its block in the last start() (last_kind())
   bool pending_ = false;
   int root_ = 0;
   int used_ = 0;  // copy streams used by the pending gather

@@ -154,6 +154,61 @@ def scenario_gather_vmm(big_mib):
     print(f"rank {me} gather vmm OK", flush=True)
 
 
+def scenario_gather_dmabuf(big_mib):
+    """gather_ of ordinary (torch / hipMalloc) blocks above the IPC limit:
+    each rank's allocation is exported as a dma-buf and pulled in place
+    (csrc/gather.cpp; IGG_GATHER_DMABUF=0: the VMM staging copy). Three
+    gathers: a first one, the same array with new values (the root's mapping
+    is reused), and a new array after the old one was freed back to the runtime
+    (a new buffer id: a new export). Every block is checked; the times printed."""
+    import time
+
+    device = _device("gpu")
+    me, dims, nprocs, coords, comm = igg.init_global_grid(8, 8, 8, quiet=True, select_device=False,
+                                                          device_type="AMDGPU")
+    nx = max(1, (int(big_mib) << 20) // (512 * 512 * 4))
+    shape = (nx, 512, 512)
+
+    def fill(A, k, p):
+        A.copy_(torch.arange(A.numel(), dtype=torch.float32, device=device).view(A.shape) % 1000003
+                + 1e7 * (p + 1) + 1e8 * k)
+
+    G = torch.zeros([int(dims[d]) * shape[d] for d in range(3)], dtype=torch.float32, device=device) \
+        if me == 0 else None
+    A = torch.empty(shape, dtype=torch.float32, device=device)
+    times = []
+    for k in range(3):
+        if k == 2:  # free the array back to the runtime and allocate a new one
+            del A
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            A = torch.empty(shape, dtype=torch.float32, device=device)
+        fill(A, k, me)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        igg.gather_(A, G, root=0)
+        torch.cuda.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+        from igg.parallel import gather as _g
+
+        kinds = comm.all_gather_object(_g._sync_puller.last_kind)
+        want = "dmabuf" if os.environ.get("IGG_GATHER_DMABUF", "1") != "0" else "vmm-staging"
+        assert kinds[1:] == [want] * (nprocs - 1), f"gather {k}: blocks published as {kinds}, expected {want}"
+        if me == 0:
+            for p in range(nprocs):
+                c = igg.native.cart_coords(p, dims.tolist())
+                blk = G[c[0] * shape[0]:(c[0] + 1) * shape[0], c[1] * shape[1]:(c[1] + 1) * shape[1],
+                        c[2] * shape[2]:(c[2] + 1) * shape[2]]
+                ref = torch.empty_like(blk)
+                fill(ref, k, p)
+                assert torch.equal(blk, ref), f"gather {k}: block of rank {p} wrong"
+                del ref
+    if me == 0:
+        print(f"gather dmabuf {big_mib} MiB per rank ({kinds[1]}): ms {[round(t, 2) for t in times]}", flush=True)
+    igg.finalize_global_grid()
+    print(f"rank {me} gather dmabuf OK", flush=True)
+
+
 def scenario_gather_regrow():
     """gather_ (IPC pull of staged chunks, IGG_GATHER_CHUNK_BYTES set by the
     test) of blocks whose chunks are MiB-sized dedicated allocations and grow
