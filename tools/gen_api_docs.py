@@ -24,11 +24,12 @@ SECTIONS = [
      ["nx_g", "ny_g", "nz_g", "x_g", "y_g", "z_g", "coords_g", "tic", "toc"]),
     ("Checkpoint / restart", "igg", ["save_checkpoint", "load_checkpoint"]),
     ("Halo engine knobs", "igg.parallel.halo",
-     ["set_transport", "set_halo_mode", "halo_mode", "set_pack_mode", "pack_mode", "enable_loopback",
-      "sendranges", "recvranges", "halosize", "free_update_halo_buffers"]),
+     ["set_transport", "transport_name", "tuned_transports", "set_halo_mode", "halo_mode", "set_pack_mode",
+      "pack_mode", "enable_loopback", "sendranges", "recvranges", "halosize", "free_update_halo_buffers"]),
     ("Stencil ops", "igg.ops.stencil", ["diffusion3d_", "diffusion3d_reference", "time_variants", "autotune"]),
     ("Applications", "igg.models.diffusion3d", ["Diffusion3D"]),
     ("", "igg.models.acoustic2d", ["Acoustic2D"]),
+    ("Field placement", "igg.utils.placement", ["candidate_count", "time_candidates", "placed"]),
     ("Tracing", "igg.utils.trace", None),
     ("Launcher", "igg.utils.launch", ["launch", "main"]),
 ]
