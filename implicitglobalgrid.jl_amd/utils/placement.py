@@ -16,14 +16,15 @@ So a model allocates ``CANDIDATES`` carves side by side, times a short
 ping-pong sweep of its own kernel on each, keeps the fastest and frees the
 rest. If all of them are alike (within ``SPREAD``) it cannot tell a box of
 only slow pages from one of only fast pages, so it allocates more, another
-batch at a time, up to ``MAX_CANDIDATES`` or half the free device memory, and
+batch at a time, up to ``MAX_CANDIDATES`` or ``MEMORY_SHARE`` of the free device
+memory, and
 stops as soon as a batch shows two speeds. ``IGG_FIELD_PLACEMENT=<k>`` probes
 exactly k candidates; ``1`` turns the probe off. The probe is also off in
 three cases:
 
 * fields under ``MIN_FIELD_BYTES``;
 * ranks that share a GPU: their probes would time each other;
-* candidates that would not fit in half the free device memory.
+* candidates that would not fit in ``MEMORY_SHARE`` of the free device memory.
 
 The reference has no counterpart: Julia arrays are allocated once by the
 application (examples/diffusion3D_multigpu_CuArrays_novis.jl:24-31).
@@ -38,6 +39,10 @@ CANDIDATES = 16
 MAX_CANDIDATES = 64
 SPREAD = 1.025  # fast and slow carves differ by 4.5-6 %; the noise of one probe is < 0.5 %
 MIN_FIELD_BYTES = 256 << 20
+# Share of the free device memory the candidates may hold while they are
+# timed (all but the chosen one are freed before the model allocates anything
+# else): 1024^3 f32 carves are 12 GiB, so on a 288 GB GPU this allows 16.
+MEMORY_SHARE = 0.75
 
 
 def candidate_count(gg, field_bytes: int, carve_bytes: int, device):
@@ -54,7 +59,7 @@ def candidate_count(gg, field_bytes: int, carve_bytes: int, device):
         if _shared_device(gg.comm):
             return 1, 1
     free, _ = torch.cuda.mem_get_info(device)
-    fit = max(1, int(free * 0.5) // max(1, carve_bytes))
+    fit = max(1, int(free * MEMORY_SHARE) // max(1, carve_bytes))
     limit = min(fit, k if env is not None else MAX_CANDIDATES)
     return min(k, limit), limit
 

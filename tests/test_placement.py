@@ -89,7 +89,9 @@ def test_candidate_count_is_off_when_ranks_share_a_gpu(monkeypatch):
     big = 1 << 30
     assert PL.candidate_count(g, big, 3 * big, torch.device("cuda", 0)) == (1, 1)
     g.comm = _Comm([(host, 0), (host, 1)])
-    assert PL.candidate_count(g, big, 3 * big, torch.device("cuda", 0)) == (PL.CANDIDATES, 48)  # 144 GiB / 3 GiB
+    assert PL.candidate_count(g, big, 3 * big, torch.device("cuda", 0)) == (PL.CANDIDATES, PL.MAX_CANDIDATES)
+    g.comm = _Comm([(host, 0), (host, 1)])
+    assert PL.candidate_count(g, 4 * big, 12 * big, torch.device("cuda", 0)) == (PL.CANDIDATES, 18)  # 216 / 12 GiB
     monkeypatch.setenv("IGG_FIELD_PLACEMENT", "5")
     assert PL.candidate_count(g, big, 3 * big, torch.device("cuda", 0)) == (5, 5)  # an explicit count: no escalation
 
