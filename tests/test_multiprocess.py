@@ -155,12 +155,12 @@ def test_diffusion_overlap_graph_two_side_streams(queues):
 @pytest.mark.parametrize("late", [False, True])
 def test_rccl_bootstrap_is_bounded_and_collective(late):
     """Two ranks on one GPU: RCCL refuses the duplicate device (an asynchronous
-    error of the non-blocking bootstrap); with rank 1 arriving 12 s late, rank
-    0's bootstrap times out after IGG_FIRST_CONTACT_TIMEOUT = 5 s and is
+    error of the non-blocking bootstrap); with rank 1 arriving 7 s late, rank
+    0's bootstrap times out after IGG_FIRST_CONTACT_TIMEOUT = 3 s and is
     aborted. Either way every rank raises the same error, none hangs."""
-    env = {"IGG_FIRST_CONTACT_TIMEOUT": "5"}
+    env = {"IGG_FIRST_CONTACT_TIMEOUT": "3"}
     if late:
-        env["IGG_INJECT_HANG"] = "rccl_init@1:12"
+        env["IGG_INJECT_HANG"] = "rccl_init@1:7"
     run_ranks(2, "rccl_init_bounded", 40 if late else 30, env_extra=env, timeout=120)
 
 
