@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "igg/devmath.hpp"
@@ -885,7 +886,13 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   const int rounds = d.rounds > 0 ? d.rounds : 1;
   // FEAT 1024: one workgroup per CU, enforced with an unused dynamic LDS
   // allocation (isolates the occupancy effect of the lower-VGPR FEAT 512 form).
-  const size_t lds = (FEAT & 1024) ? 96 * 1024 : 0;
+  size_t lds = (FEAT & 1024) ? 96 * 1024 : 0;
+  // Measurement knob: IGG_HX_WG_PER_CU=k caps the resident workgroups per CU at
+  // k (dynamic LDS of 160 KiB / k), which also sizes the chunks of the grid.
+  if (const char* e = std::getenv("IGG_HX_WG_PER_CU"); e && (FEAT & 1024) == 0) {
+    const int k = std::atoi(e);
+    if (k > 0) lds = std::max<size_t>(lds, (160 * 1024) / static_cast<size_t>(k) - 1024);
+  }
   const int64_t target = static_cast<int64_t>(rounds) * resident(reinterpret_cast<const void*>(kern), block, lds);
   const int64_t ch_all = std::max<int64_t>(1, (len0 * tiles + target - 1) / target);
   const int64_t nch = std::max<int64_t>(1, (len0 + ch_all - 1) / ch_all);
