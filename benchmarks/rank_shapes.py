@@ -34,7 +34,7 @@ import torch  # noqa: E402
 import igg  # noqa: E402
 from igg._native import native  # noqa: E402
 
-PLAIN = (2, 11, 14, 21, 24, 26, 40, 43)  # ops/stencil.py SHORTLIST
+PLAIN = (2, 11, 14, 21, 24, 26, 40, 43, 44)  # ops/stencil.py SHORTLIST
 ROUNDS = (1, 2, 3)
 # bench.py FUSED_CANDIDATES / FUSED_DIRECT / FUSED_DIRECT_F32 (+ peel bit 8)
 FUSED = ((0, 0, 3), (0, 1, 3), (0, 0, 1), (9, 0, 3), (14, 0, 3), (40, 0, 2), (42, 0, 2), (42, 1, 2), (50, 0, 2),

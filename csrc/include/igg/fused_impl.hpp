@@ -225,6 +225,10 @@ constexpr int ZLO = 524288, ZHI = 1048576, ZSIDES = 2097152;
 // RY <= 16, one z edge per wave, and zh % 16 >= RY - 1 (launch_mode checks;
 // otherwise the readlane form runs).
 constexpr int ZDPP = 4194304;
+// OCC2 (round 6, launch only): at most 2 workgroups per CU, enforced with an
+// unused dynamic LDS allocation as FEAT 1024 does for one; the grid's chunks are
+// sized for that residency. f32 tiling 0 gains 2.5 % (plain variant 44).
+constexpr int OCC2 = 8388608;
 
 template <typename T, int BY, int RY, int VZ, bool PF, int BZ, bool DF, int FEAT>
 __device__ __forceinline__ void
@@ -886,7 +890,7 @@ void launch_hx(const DiffusionArgs& d, const HaloIOArgs& io, hipStream_t stream,
   const int rounds = d.rounds > 0 ? d.rounds : 1;
   // FEAT 1024: one workgroup per CU, enforced with an unused dynamic LDS
   // allocation (isolates the occupancy effect of the lower-VGPR FEAT 512 form).
-  size_t lds = (FEAT & 1024) ? 96 * 1024 : 0;
+  size_t lds = (FEAT & 1024) ? 96 * 1024 : ((FEAT & OCC2) ? 79 * 1024 : 0);
   // Measurement knob: IGG_HX_WG_PER_CU=k caps the resident workgroups per CU at
   // k (dynamic LDS of 160 KiB / k), which also sizes the chunks of the grid.
   if (const char* e = std::getenv("IGG_HX_WG_PER_CU"); e && (FEAT & 1024) == 0) {

@@ -18,7 +18,7 @@ namespace {
 template <typename T>
 void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
   const HaloIOArgs none{};
-  switch (v) {  // tilings of the shortlisted restrict-form variants 21/24/26/40/43
+  switch (v) {  // tilings of the shortlisted restrict-form variants 21/24/26/40/43/44
     // each tiling in the partial-line and the whole-line (HZ, halo_z) z-edge
     // store form: the autotune times both (models/diffusion3d.py)
 #define IGG_PLAIN_HX(BY, RY, VZ, BZ, F)                                         \
@@ -29,6 +29,7 @@ void dispatch_plain(const DiffusionArgs& d, int v, hipStream_t s) {
     case 100: IGG_PLAIN_HX(2, 8, 2, 1, 0); break;
     case 124: IGG_PLAIN_HX(4, 8, 2, 1, 512 | 1024); break;
     case 141: IGG_PLAIN_HX(2, 8, 2, 4, 0); break;
+    case 150: IGG_PLAIN_HX(4, 4, 4, 1, OCC2); break;
 #ifdef IGG_PROBES
     // restrict forms of tilings 9 and 14 (variants 23, 25): no A/B win in rounds 2-4
     case 9: IGG_PLAIN_HX(4, 8, 4, 1, 0); break;

@@ -350,11 +350,14 @@ constexpr Variant VARIANTS[] = {
     {"hx_v2_by4_ry12_nt_zl_occ1", 4, 12, 2, false, true}, // 42
     // 43: full-row z tiles (BZ 4 x 64 lanes x VZ 2 = 512 points, profiles/r2_fullrow/)
     {"hx_v2_bz4_by2_ry8_nt", 2, 8, 2, false, true},     // 43
+    // 44: tiling 0 at most 2 workgroups per CU (f32 1024^3: 2.5 % ahead of its
+    // 3-per-CU form, profiles/r6_vsweep/)
+    {"hx_v4_by4_ry4_nt_occ2", 4, 4, 4, false, true},    // 44
 };
 // Variants 21..31: restrict-form tiling id (fused_kernels.hip dispatch_plain)
 // and the stencil_kernels.hip variant used for boxes other than the inner box.
-constexpr int HX_TILING[] = {0, 2, 9, 11, 14, 100, 101, 102, 103, 104, 105, 110, 111, 112, 113, 120, 121, 122, 123, 124, 125, 126, 141};
-constexpr int HX_FALLBACK[] = {0, 2, 9, 11, 14, 11, 11, 11, 2, 5, 11, 11, 0, 9, 14, 11, 9, 11, 0, 11, 11, 11, 11};
+constexpr int HX_TILING[] = {0, 2, 9, 11, 14, 100, 101, 102, 103, 104, 105, 110, 111, 112, 113, 120, 121, 122, 123, 124, 125, 126, 141, 150};
+constexpr int HX_FALLBACK[] = {0, 2, 9, 11, 14, 11, 11, 11, 2, 5, 11, 11, 0, 9, 14, 11, 9, 11, 0, 11, 11, 11, 11, 0};
 constexpr int NVARIANTS = sizeof(VARIANTS) / sizeof(VARIANTS[0]);
 
 // Grid sizing policy: `g_rounds` full residency rounds (resident workgroups =
@@ -523,7 +526,7 @@ bool stencil_variant_compiled(int v) {
 #else
   switch (v) {
     case 0: case 1: case 2: case 5: case 9: case 11: case 14: case 18:
-    case 21: case 24: case 26: case 40: case 43:
+    case 21: case 24: case 26: case 40: case 43: case 44:
       return true;
     default:
       return false;

@@ -76,7 +76,8 @@ def _variant_for(T, boxes, rd2, dtlam, T2, Cp, stream) -> int:
 # form; 40: lane-distributed z-segment edge loads at one workgroup per CU
 # (profiles/r1_zl/); 43: full-row z tiles (profiles/r2_fullrow/). 0, 9, 23 and
 # 25 never won a real config in rounds 2-4 (23/25 are --probes builds now).
-SHORTLIST = (2, 11, 14, 21, 24, 26, 40, 43)
+# 44 (round 6): tiling 0 at 2 workgroups per CU (f32, profiles/r6_vsweep/).
+SHORTLIST = (2, 11, 14, 21, 24, 26, 40, 43, 44)
 # Grid residency rounds tried per variant by the model autotune: 1-4 measured
 # best depending on the box and variant (profiles/r1_fused/grid.log,
 # variant_sweep.log, r1_zl/: 1-2.5 %).
