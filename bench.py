@@ -849,7 +849,11 @@ def _fused_check(model, comm, log, nchk: int = FUSED_CHECK_STEPS, inject: str = 
     ov = bool(getattr(model, "overlap", False))
     if ov:
         model.set_overlap(False)
-    saved = {n: getattr(model, n).clone() for n in names}
+    # The state to restore: on the host when ranks share one GPU (8 ranks of
+    # 1024^3 f32 ran out of the shared device memory with it on the device:
+    # 8 x 8 GiB, profiles/r6_checks/rehearsals/).
+    host = bool(_BRACKET.get("shared"))
+    saved = {n: (getattr(model, n).to("cpu") if host else getattr(model, n).clone()) for n in names}
 
     def restore():
         for n in names:
@@ -1270,6 +1274,7 @@ def main():
     os.environ.setdefault("IGG_PUT_TIMEOUT", "20")
     if args.share_gpu:
         os.environ.setdefault("IGG_TRANSPORT", "staged")
+        _BRACKET["shared"] = True  # the ranks' device memory is one pool (_fused_check keeps its copy on the host)
     # The bench validates and A/B-times the transports itself (validate_transports,
     # select_transport below): the library's own first-exchange choice
     # (IGG_TRANSPORT=auto) stays out of the model setup before them.

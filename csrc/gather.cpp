@@ -100,12 +100,16 @@ uint32_t get_u32(const std::string& r, size_t at) {
 
 }  // namespace
 
-// IGG_GATHER_VMM=0: large snapshots go through IPC staging chunks (rounds
-// 3-5) instead of one VMM staging buffer.
+// IGG_GATHER_VMM=1: large snapshots go through ONE VMM staging buffer
+// instead of IPC staging chunks (rounds 3-5). Off by default: allocated on the
+// first gather of a running job (hipMemCreate + map while this process's
+// kernels run), it ended in an illegal-address error in an 8-rank 1024^3 f32
+// run on one GPU (profiles/r6_vmm/NOTES.md), and it was no faster than the
+// chunks (4.10 vs 3.83 ms).
 bool vmm_staging() {
   static const bool on = [] {
     const char* e = std::getenv("IGG_GATHER_VMM");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

@@ -120,10 +120,18 @@ def _check_and_time(fields, names, switch, comm, rank: int, nranks: int, ref, st
             continue
         if ref is None and first_ok is None:
             first_ok = [x.clone() for x in X]
-        probes[name] = X  # timed below on the probes (the caller's fields stay untouched)
+        # timed below on ONE probe set shared by the candidates (the caller's
+        # fields stay untouched; probes per candidate would hold that many
+        # field-sized copies, which ranks sharing a GPU ran out of memory on)
+        if not probes:
+            Xt = X
+        probes[name] = True
+        del X
+    del first_ok
     n = max(1, int(steps))
     for _ in range(max(1, int(rounds))):
-        for name, X in probes.items():
+        for name in probes:
+            X = Xt
             (reswitch or switch)(name)
             _halo.update_halo_(*X)  # warm: the switch may have left another transport's state behind
             torch.cuda.synchronize()
@@ -135,6 +143,10 @@ def _check_and_time(fields, names, switch, comm, rank: int, nranks: int, ref, st
             torch.cuda.synchronize()
             dt = _agree_max(comm, time.perf_counter() - t0)
             ms[name] = min(ms.get(name, float("inf")), round(dt / n * 1e3, 5))
+    if probes:
+        del X, Xt
+    # the probes' memory back to the device (other processes may share it)
+    torch.cuda.empty_cache()
     return checked, ms
 
 

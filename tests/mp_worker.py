@@ -157,7 +157,7 @@ def scenario_gather_vmm(big_mib):
 def scenario_gather_dmabuf(big_mib):
     """gather_ of ordinary (torch / hipMalloc) blocks above the IPC limit:
     each rank's allocation is exported as a dma-buf and pulled in place
-    (csrc/gather.cpp; IGG_GATHER_DMABUF=0: the VMM staging copy). Three
+    (csrc/gather.cpp; IGG_GATHER_DMABUF=0: staged copies). Three
     gathers: a first one, the same array with new values (the root's mapping
     is reused), and a new array after the old one was freed back to the runtime
     (a new buffer id: a new export). Every block is checked; the times printed."""
@@ -192,7 +192,8 @@ def scenario_gather_dmabuf(big_mib):
         from igg.parallel import gather as _g
 
         kinds = comm.all_gather_object(_g._sync_puller.last_kind)
-        want = "dmabuf" if os.environ.get("IGG_GATHER_DMABUF", "1") != "0" else "vmm-staging"
+        want = ("dmabuf" if os.environ.get("IGG_GATHER_DMABUF", "1") != "0"
+                else "vmm-staging" if os.environ.get("IGG_GATHER_VMM") == "1" else "chunks")
         assert kinds[1:] == [want] * (nprocs - 1), f"gather {k}: blocks published as {kinds}, expected {want}"
         if me == 0:
             for p in range(nprocs):

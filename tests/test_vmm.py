@@ -51,15 +51,16 @@ def test_gather_pulls_vmm_blocks_and_stages_large_snapshots_in_one_buffer():
     """gather_ maps blocks in VMM memory in place at any size and stages a
     large snapshot (1.1 GiB per rank here) into one VMM buffer instead of IPC
     chunks; three ranks sharing a GPU, every block checked."""
-    run_ranks(3, "gather_vmm", 1100, env_extra={"IGG_FIRST_CONTACT_TIMEOUT": "60"}, timeout=170)
+    run_ranks(3, "gather_vmm", 1100, env_extra={"IGG_FIRST_CONTACT_TIMEOUT": "60", "IGG_GATHER_VMM": "1"},
+              timeout=170)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dmabuf", ["1", "0"])
 def test_gather_pulls_large_ordinary_blocks(dmabuf):
     """gather_ of torch blocks of 2.1 GiB per rank (above the IPC limit): as a
-    dma-buf of the allocation, in place (default), or through the VMM staging
-    copy (IGG_GATHER_DMABUF=0); the same array again with new values, then a new
+    dma-buf of the allocation, in place (default), or staged into IPC chunks
+    (IGG_GATHER_DMABUF=0); the same array again with new values, then a new
     allocation after the old one was freed; every block checked."""
     outs = run_ranks(2, "gather_dmabuf", 2200, env_extra={"IGG_FIRST_CONTACT_TIMEOUT": "60",
                                                           "IGG_GATHER_DMABUF": dmabuf}, timeout=170)
