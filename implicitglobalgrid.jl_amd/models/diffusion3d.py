@@ -30,7 +30,6 @@ bitwise identical to the update_halo_ path.
 """
 from __future__ import annotations
 
-import math
 import os
 import warnings
 
